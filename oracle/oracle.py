@@ -1,0 +1,167 @@
+"""ctypes front-end of the CPU restatement in hg_oracle.c.
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product package.  Parity of every
+function here is pinned by tests/test_oracle_golden.py against golden vectors
+captured from the reference (tests/golden/make_golden.py).
+
+Each function mirrors one reference entry point (paths under /root/reference):
+  rect_to_hex   HyGrid/geometry_np.py:358-519
+  hex_to_rect   HyGrid/geometry_np.py:191-356 (linear); nearest per
+                HyGrid/geometry_torch.py:335-347
+  hexresize     HyGrid/geometry_np.py:520-681
+  hexconv2d     HyGrid/HexFrames.py:96-169
+Inputs are (planes, h, w) arrays of any real dtype; outputs are float64.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libhg_oracle.so")
+_lib = None
+
+_i64 = ctypes.c_int64
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int32)
+
+PAD_MODES = {"constant": 0, "zeros": 0, "reflect": 1, "replicate": 2, "circular": 3}
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.or_linspace.restype = ctypes.c_double
+        L.or_linspace.argtypes = [ctypes.c_double, ctypes.c_double, _i64, _i64]
+        for name in ("or_r2h_maps", "or_h2r_maps", "or_hexresize_maps"):
+            getattr(L, name).argtypes = [_i64] * 4 + [_ip, _dp]
+            getattr(L, name).restype = None
+        for name in ("or_rect_to_hex", "or_hex_to_rect", "or_hexresize"):
+            getattr(L, name).argtypes = [_dp, _dp] + [_i64] * 5 + [ctypes.c_int]
+            getattr(L, name).restype = None
+        L.or_hexconv2d_out_shape.argtypes = [_i64, _i64] + [ctypes.c_int] * 4 + [
+            ctypes.POINTER(_i64), ctypes.POINTER(_i64)]
+        L.or_hexconv2d.argtypes = [_dp, _dp, _dp, _dp] + [_i64] * 5 + [ctypes.c_int] * 7 + [
+            ctypes.c_double]
+        L.or_heximage_to_type1.argtypes = [_dp, _dp, _i64, _i64, _i64, ctypes.c_int]
+        L.or_heximage_to_type1.restype = None
+        L.or_num_threads.restype = ctypes.c_int
+        L.or_set_num_threads.argtypes = [ctypes.c_int]
+        L.or_set_num_threads.restype = None
+        _lib = L
+    return _lib
+
+
+def set_num_threads(n):
+    lib().or_set_num_threads(int(n))
+
+
+def num_threads():
+    return lib().or_num_threads()
+
+
+def _dptr(a):
+    return a.ctypes.data_as(_dp)
+
+
+def _as_planes(x):
+    x = np.ascontiguousarray(np.asarray(x), dtype=np.float64)
+    if x.ndim == 2:
+        x = x[None]
+    return x.reshape(-1, x.shape[-2], x.shape[-1]), x.shape[:-2]
+
+
+def linspace(start, stop, n):
+    return np.array([lib().or_linspace(start, stop, n, k) for k in range(n)])
+
+
+def _maps(fn, nf, h, w, h1, w1):
+    im = np.zeros((5, h1, w1), np.int32)
+    fm = np.zeros((nf, h1, w1), np.float64)
+    fn(h, w, h1, w1, im.ctypes.data_as(_ip), _dptr(fm))
+    keys = ("i_n", "j_n", "flag", "valid", "argmin")
+    out = {k: im[i] for i, k in enumerate(keys)}
+    fkeys = ("i_f", "j_f", "alpha", "beta", "gamma")[:nf]
+    out.update({k: fm[i] for i, k in enumerate(fkeys)})
+    return out
+
+
+def r2h_maps(h, w, h1, w1):
+    return _maps(lib().or_r2h_maps, 2, h, w, h1, w1)
+
+
+def h2r_maps(h, w, h1, w1):
+    return _maps(lib().or_h2r_maps, 5, h, w, h1, w1)
+
+
+def hexresize_maps(h, w, h1, w1):
+    return _maps(lib().or_hexresize_maps, 5, h, w, h1, w1)
+
+
+def _resample(fn, x, size, interp):
+    planes, lead = _as_planes(x)
+    n, h, w = planes.shape
+    h1, w1 = (h, w) if size is None else size
+    out = np.empty((n, h1, w1), np.float64)
+    fn(_dptr(planes), _dptr(out), n, h, w, h1, w1, int(interp))
+    return out.reshape(tuple(lead) + (h1, w1))
+
+
+def rect_to_hex(x, size=None, interp=1):
+    return _resample(lib().or_rect_to_hex, x, size, interp)
+
+
+def hex_to_rect(x, size=None, interp=1):
+    return _resample(lib().or_hex_to_rect, x, size, interp)
+
+
+def hexresize(x, size, interp=1):
+    return _resample(lib().or_hexresize, x, size, interp)
+
+
+def hexconv2d_out_shape(h, w, r, stride=1, padding=0, dilation=1):
+    ho, wo = _i64(), _i64()
+    st = lib().or_hexconv2d_out_shape(h, w, r, stride, padding, dilation, ctypes.byref(ho),
+                                      ctypes.byref(wo))
+    if st:
+        raise ValueError(f"hexconv2d: input too small or bad params (status {st})")
+    return ho.value, wo.value
+
+
+def hexconv2d(x, kernel, bias, even_odd_offset, radius, stride=1, padding=0, dilation=1,
+              groups=1, padding_mode="constant", padding_value=0.0):
+    x = np.ascontiguousarray(x, np.float64)
+    while x.ndim < 4:
+        x = x[None]
+    B, C, h, w = x.shape
+    k = np.ascontiguousarray(kernel, np.float64)
+    O = k.shape[0]
+    ho, wo = hexconv2d_out_shape(h, w, radius, stride, padding, dilation)
+    y = np.empty((B, O, ho, wo), np.float64)
+    bp = None
+    if bias is not None:
+        bias = np.ascontiguousarray(bias, np.float64)
+        bp = _dptr(bias)
+    st = lib().or_hexconv2d(_dptr(x), _dptr(k), bp, _dptr(y), B, C, O, h, w, radius, stride,
+                            padding, dilation, groups, int(even_odd_offset),
+                            PAD_MODES[padding_mode], float(padding_value))
+    if st:
+        raise ValueError(f"hexconv2d oracle status {st}")
+    return y
+
+
+def heximage_to_type1(x, even_odd_offset):
+    planes, lead = _as_planes(x)
+    n, h, w = planes.shape
+    t = np.empty((n, h, 2 * w + 1), np.float64)
+    lib().or_heximage_to_type1(_dptr(planes), _dptr(t), n, h, w, int(even_odd_offset))
+    return t.reshape(tuple(lead) + (h, 2 * w + 1))
