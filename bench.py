@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path on BASELINE.json's headline workload.
+
+Workload (BASELINE.json configs[2], "config 3"): per GPU a batch of 128 4K RGB
+rasters (3 x 2160 x 3840, bf16, synthetic U[0,1), seed 2+rank), one step =
+rect->hex bilinear resample (2160x3840) -> HexConv2d(3, 3, even_odd_offset=0,
+radius 2, padding=1, bias; weights drawn with torch.manual_seed(3) and the
+reference initialiser) -> hex->rect linear resample (2160x3840), all on the
+gfx950 kernels of libhygrid_hip.so, with bf16 tensors between stages.
+
+Multi-GPU: one process per GPU (torchrun); every rank owns its own 128 images
+(weak scaling, no data-path collective).  value = all ranks' input pixels / the
+max-over-ranks wall time of K steps.  After the timed region, per-image
+checksums are all-gathered over RCCL, and (N>1) the full-output gather to rank 0
+is timed and reported on its own (`gather`), never folded into `value`.
+
+Extra JSON fields: `kernels` (per-stage HIP-event times and algorithmic GB/s),
+`roofline` (dominant kernel vs 8 TB/s HBM), `cpu_baseline` (the C/OpenMP oracle
+restatement on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "hybrid-grid-for-hexagonal-and-rectangular-image-processing_amd")
+for _p in (ROOT, PKG_DIR):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=128, help="images per GPU")
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--channels", type=int, default=3)
+    ap.add_argument("--cpu-images", type=int, default=64,
+                    help="max images in the CPU-baseline sample (~10 s; 0 disables it)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--no-gather", action="store_true", help="skip the timed output gather")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="per-kernel HBM bytes from rocprofv3 PMC passes (optional)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, kernel, bias):
+    """Oracle (C/OpenMP fp64 restatement) on a bounded sample of the same workload:
+    whole images, one at a time, until ~10 s of CPU work (at most --cpu-images)."""
+    import numpy as np
+
+    from oracle import oracle as O
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    O.set_num_threads(threads)
+    rng = np.random.default_rng(2)
+    x = rng.random((1, args.channels, args.height, args.width))
+    n, dt = 0, 0.0
+    while n < args.cpu_images and (n == 0 or dt < 10.0):
+        t0 = time.perf_counter()
+        hexim = O.rect_to_hex(x, (args.height, args.width), 1)
+        c = O.hexconv2d(hexim, kernel, bias, 0, 2, padding=1)
+        O.hex_to_rect(c, (args.height, args.width), 1)
+        dt += time.perf_counter() - t0
+        n += 1
+    return {"value": round(n * args.height * args.width / dt / 1e6, 3), "unit": "Mpix/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{n} image(s) of {args.channels}x{args.height}x{args.width}, one at a "
+                      f"time (fp64 oracle/hg_oracle.c, r2h->HexConv2d->h2r), {dt:.2f} s"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    from HyGrid import ops
+    from HyGrid.HexFrames import HexConv2d
+
+    B, C, H, W = args.batch, args.channels, args.height, args.width
+    bf16 = torch.bfloat16
+    gen = torch.Generator(device=dev).manual_seed(2 + rank)
+    x = torch.rand((B, C, H, W), generator=gen, device=dev, dtype=bf16)
+    torch.manual_seed(3)
+    conv = HexConv2d(C, C, 0, 2, padding=1, groups=1, bias=True).to(dev)
+    conv.out_dtype = bf16
+
+    stages = ("rect_to_hex", "hexconv2d", "hex_to_rect")
+    ev = []
+
+    def step(record):
+        if record:
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            e[0].record()
+        h = ops.rect_to_hex(x, (H, W), out_dtype=bf16)
+        if record:
+            e[1].record()
+        c = conv(h)
+        if record:
+            e[2].record()
+        y = ops.hex_to_rect(c, (H, W), out_dtype=bf16)
+        if record:
+            e[3].record()
+            ev.append(e)
+        return y
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            y = step(False)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            y = step(True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    mpix = world * B * H * W * args.steps / elapsed / 1e6
+
+    # per-stage kernel times (HIP events on the launch stream, timed region only)
+    stage_ms = {s: sum(e[i].elapsed_time(e[i + 1]) for e in ev) / len(ev)
+                for i, s in enumerate(stages)}
+    elem = 2  # bf16 bytes
+    alg_bytes = {s: 2 * B * C * H * W * elem for s in stages}   # read once + write once
+    kernels = {s: {"ms": round(stage_ms[s], 4), "alg_GB": round(alg_bytes[s] / 1e9, 4),
+                   "GB_per_s": round(alg_bytes[s] / (stage_ms[s] * 1e-3) / 1e9, 1)}
+               for s in stages}
+    dom = max(stages, key=lambda s: stage_ms[s])
+    achieved = alg_bytes[dom] / (stage_ms[dom] * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            with open(args.pmc_json) as f:
+                pmc = json.load(f)
+            if dom in pmc.get("kernels", {}):
+                traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"]
+        except Exception as exc:  # keep the bench line even if the file is malformed
+            log("pmc json unreadable:", exc)
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "alg_bytes_per_launch": alg_bytes[dom]}
+
+    # checksums over RCCL (not timed), and the full-output gather on its own
+    from HyGrid.dist import gather_checksums, gather_to_root, image_checksums
+    cs = image_checksums(y)
+    gather = None
+    if world > 1:
+        cs = gather_checksums(cs)
+        if not args.no_gather:
+            try:
+                gather_to_root(y)            # warm the RCCL channels
+                torch.cuda.synchronize()
+                dist.barrier()
+                g0 = time.perf_counter()
+                out = gather_to_root(y)
+                torch.cuda.synchronize()
+                g1 = time.perf_counter()
+                del out
+                gb = (world - 1) * y.numel() * y.element_size() / 1e9
+                gather = {"GB_into_root": round(gb, 3), "ms": round((g1 - g0) * 1e3, 3),
+                          "GB_per_s": round(gb / (g1 - g0), 1),
+                          "xgmi_ingress_bound_GB_per_s": round(min(world - 1, 7) * 153.0, 1)}
+            except Exception as exc:
+                log("gather failed:", exc)
+    checksum = float(cs[..., 0].sum().item())
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_images > 0:
+        try:
+            cpu = cpu_baseline(args, conv.kernel.detach().cpu().numpy(),
+                               conv.bias.detach().cpu().numpy())
+        except Exception as exc:
+            log("cpu baseline failed:", exc)
+
+    if rank == 0:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            metric = json.load(f)["metric"]
+        line = {
+            "metric": metric, "value": round(mpix, 1), "unit": "Mpix/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": f"synthetic U[0,1) bf16 rasters generated on device, seed 2+rank; "
+                    f"HexConv2d weights torch.manual_seed(3) + reference init",
+            "config": {"workload": "config3: 4K RGB batch=128/GPU, rect->hex bilinear -> "
+                                   "HexConv2d(3,3,off=0,r=2,pad=1) -> hex->rect linear",
+                       "batch_per_gpu": B, "global_batch": B * world, "channels": C,
+                       "height": H, "width": W, "parallelism": f"dp{world}",
+                       "fused": False},
+            "kernels": kernels, "roofline": roofline, "cpu_baseline": cpu,
+            "gather": gather, "checksum": checksum,
+            "device": torch.cuda.get_device_name(dev),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

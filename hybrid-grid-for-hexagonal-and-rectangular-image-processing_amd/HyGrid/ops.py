@@ -1,0 +1,131 @@
+"""Tensor-level entry points: torch device tensors in, torch device tensors out.
+
+Thin layer over the C ABI (`_abi`): shape/dtype policy, output allocation (the
+caller — here torch's caching allocator — owns every buffer), and the current
+HIP stream.  The reference-compatible surfaces (geometry_np, geometry_torch,
+HexFrames, ...) are built on these.
+
+Layout: a raster batch is any tensor (..., H, W); all leading dims are flattened
+into `planes`, which the kernels walk with the lattice maps computed once.
+"""
+import ctypes
+
+import torch
+
+from . import _abi
+
+_FLOATS = (torch.float16, torch.bfloat16, torch.float32, torch.float64)
+
+
+def _planes(x):
+    if x.dim() < 2:
+        raise ValueError(f"expected a raster (..., H, W), got shape {tuple(x.shape)}")
+    x = x.contiguous()
+    lead = tuple(x.shape[:-2])
+    planes = 1
+    for d in lead:
+        planes *= d
+    return x, lead, planes
+
+
+def _resample(fn_name, x, size, interp, out_dtype):
+    _abi.require_device(x)
+    x, lead, planes = _planes(x)
+    h, w = int(x.shape[-2]), int(x.shape[-1])
+    h1, w1 = (h, w) if size is None else (int(size[0]), int(size[1]))
+    if interp == _abi.HG_NEAREST:
+        out_dtype = x.dtype
+    elif out_dtype is None:
+        out_dtype = x.dtype if x.dtype in _FLOATS else torch.float32
+    y = torch.empty(lead + (h1, w1), dtype=out_dtype, device=x.device)
+    st = getattr(_abi.lib(), fn_name)(
+        _abi.ptr(x), _abi.ptr(y), _abi.dtype_code(x.dtype), _abi.dtype_code(out_dtype),
+        planes, h, w, h1, w1, int(interp), _abi.stream_of(x))
+    _abi.check(st, fn_name)
+    return y
+
+
+def rect_to_hex(x, size=None, interp=_abi.HG_LINEAR, out_dtype=None):
+    """rect (..., H, W) -> hex (..., H1, W1); geometry_np.py:358-519."""
+    return _resample("hg_rect_to_hex", x, size, interp, out_dtype)
+
+
+def hex_to_rect(x, size=None, interp=_abi.HG_LINEAR, out_dtype=None):
+    """hex (..., H, W) -> rect (..., H1, W1); geometry_np.py:191-356."""
+    return _resample("hg_hex_to_rect", x, size, interp, out_dtype)
+
+
+def hexresize(x, size, interp=_abi.HG_LINEAR, out_dtype=None):
+    """hex (..., H, W) -> hex (..., H1, W1); geometry_np.py:520-681."""
+    return _resample("hg_hexresize", x, size, interp, out_dtype)
+
+
+_OPS = {"rect_to_hex": _abi.HG_OP_RECT_TO_HEX, "hex_to_rect": _abi.HG_OP_HEX_TO_RECT,
+        "hexresize": _abi.HG_OP_HEXRESIZE}
+
+
+def lattice_maps(op, h, w, h1, w1, device=None):
+    """The integer lattice maps + fp64 coefficients a resample uses (parity tests)."""
+    device = torch.device("cuda") if device is None else torch.device(device)
+    if not torch.cuda.is_available():
+        raise RuntimeError("HyGrid needs a HIP device (MI355X); none is available.")
+    im = torch.empty((5, h1, w1), dtype=torch.int32, device=device)
+    fm = torch.empty((5, h1, w1), dtype=torch.float64, device=device)
+    st = _abi.lib().hg_lattice_maps(_OPS[op], h, w, h1, w1, _abi.ptr(im), _abi.ptr(fm),
+                                    _abi.stream_of(im))
+    _abi.check(st, "hg_lattice_maps")
+    keys = ("i_n", "j_n", "flag", "valid", "argmin")
+    out = {k: im[i] for i, k in enumerate(keys)}
+    out.update({k: fm[i] for i, k in enumerate(("i_f", "j_f", "alpha", "beta", "gamma"))})
+    return out
+
+
+def hexconv2d_out_shape(h, w, radius, stride=1, padding=0, dilation=1):
+    ho, wo = ctypes.c_int64(), ctypes.c_int64()
+    st = _abi.lib().hg_hexconv2d_out_shape(h, w, radius, stride, padding, dilation,
+                                          ctypes.byref(ho), ctypes.byref(wo))
+    _abi.check(st, "hexconv2d_out_shape")
+    return ho.value, wo.value
+
+
+def hexconv2d(x, kernel, bias, even_odd_offset, radius, stride=1, padding=0, dilation=1,
+              groups=1, padding_mode="constant", padding_value=0.0, out_dtype=None):
+    """HexConv2d forward (HexFrames.py:96-169) on (B, C, H, W) -> (B, O, Ho, Wo).
+
+    kernel: (O, C/groups, 1, K) or (O, C/groups, K) float32/float64 — the
+    accumulation dtype, as the reference's `input.to(self.kernel.dtype)` (:107).
+    """
+    _abi.require_device(x)
+    while x.dim() < 4:
+        x = x.unsqueeze(0)
+    x = x.contiguous()
+    B, C, h, w = (int(s) for s in x.shape)
+    k = kernel.detach()
+    if k.dtype not in (torch.float32, torch.float64):
+        k = k.float()
+    k = k.reshape(k.shape[0], k.shape[1], -1).contiguous()
+    O = int(k.shape[0])
+    if int(k.shape[1]) * groups != C:
+        raise ValueError(f"kernel expects {int(k.shape[1]) * groups} input channels, got {C}")
+    b = None
+    if bias is not None:
+        b = bias.detach().to(k.dtype).contiguous()
+    if out_dtype is None:
+        out_dtype = torch.get_default_dtype()
+    ho, wo = hexconv2d_out_shape(h, w, radius, stride, padding, dilation)
+    y = torch.empty((B, O, ho, wo), dtype=out_dtype, device=x.device)
+    pm = _abi.PAD_MODES.get(padding_mode)
+    if pm is None:
+        raise ValueError(f"unsupported padding_mode {padding_mode!r}")
+    st = _abi.lib().hg_hexconv2d(
+        _abi.ptr(x), _abi.ptr(k), _abi.ptr(b), _abi.ptr(y), _abi.dtype_code(x.dtype),
+        _abi.dtype_code(k.dtype), _abi.dtype_code(out_dtype), B, C, O, h, w, radius, stride,
+        padding, dilation, groups, int(even_odd_offset), pm, float(padding_value),
+        _abi.stream_of(x))
+    _abi.check(st, "hg_hexconv2d")
+    return y
+
+
+def hexconv2d_backward(gy, x, kernel, bias, cfg, need_x, need_k, need_b):
+    """Gradients of hexconv2d."""
+    raise NotImplementedError("HexConv2d backward kernels are not built yet")

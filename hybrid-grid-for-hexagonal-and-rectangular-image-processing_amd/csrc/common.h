@@ -1,0 +1,77 @@
+// common.h — dtype plumbing and launch helpers shared by the HyGrid gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hygrid.h"
+
+namespace hg {
+
+// Element types of the C-ABI dtype enum (include/hygrid.h).  bf16/f16 are the
+// compiler's native storage types: hipcc lowers (__bf16)f to v_cvt_pk_bf16_f32
+// (round-to-nearest-even, NaN kept NaN) and (float)b to a 16-bit shift.
+template <int DT> struct dtype_of;
+template <> struct dtype_of<HG_U8>   { using T = uint8_t; };
+template <> struct dtype_of<HG_I8>   { using T = int8_t; };
+template <> struct dtype_of<HG_U16>  { using T = uint16_t; };
+template <> struct dtype_of<HG_I16>  { using T = int16_t; };
+template <> struct dtype_of<HG_I32>  { using T = int32_t; };
+template <> struct dtype_of<HG_I64>  { using T = int64_t; };
+template <> struct dtype_of<HG_F16>  { using T = _Float16; };
+template <> struct dtype_of<HG_BF16> { using T = __bf16; };
+template <> struct dtype_of<HG_F32>  { using T = float; };
+template <> struct dtype_of<HG_F64>  { using T = double; };
+
+inline int dtype_size(int dt) {
+    switch (dt) {
+    case HG_U8: case HG_I8: return 1;
+    case HG_U16: case HG_I16: case HG_F16: case HG_BF16: return 2;
+    case HG_I32: case HG_F32: return 4;
+    case HG_I64: case HG_F64: return 8;
+    default: return 0;
+    }
+}
+inline bool dtype_is_float(int dt) {
+    return dt == HG_F16 || dt == HG_BF16 || dt == HG_F32 || dt == HG_F64;
+}
+
+template <typename A, typename T> __device__ __forceinline__ A to_acc(T v) { return (A)v; }
+template <typename T, typename A> __device__ __forceinline__ T from_acc(A v) { return (T)v; }
+
+// Map (in dtype, out dtype) of a floating-point kernel onto its template.
+// Integer inputs are exact in f32 up to 2^24, so the accumulator is f64 only when
+// the caller asks for f64 output or feeds f64/i32/i64 data.
+inline bool acc_is_double(int in_dt, int out_dt) {
+    return out_dt == HG_F64 || in_dt == HG_F64 || in_dt == HG_I32 || in_dt == HG_I64;
+}
+
+inline int hip_status(hipError_t e) { return e == hipSuccess ? HG_OK : (int)e; }
+
+inline int launch_status() { return hip_status(hipGetLastError()); }
+
+}  // namespace hg
+
+// Instantiate `FN<Tin, Tout>(args...)` for every supported (in, out) dtype pair.
+// The body returns HG_EDTYPE for pairs it does not support.
+#define HG_DISPATCH_IN(dt, TIN, ...)                                         \
+    switch (dt) {                                                            \
+    case HG_U8:   { using TIN = uint8_t;  __VA_ARGS__; } break;              \
+    case HG_I8:   { using TIN = int8_t;   __VA_ARGS__; } break;              \
+    case HG_U16:  { using TIN = uint16_t; __VA_ARGS__; } break;              \
+    case HG_I16:  { using TIN = int16_t;  __VA_ARGS__; } break;              \
+    case HG_I32:  { using TIN = int32_t;  __VA_ARGS__; } break;              \
+    case HG_F16:  { using TIN = _Float16; __VA_ARGS__; } break;              \
+    case HG_BF16: { using TIN = __bf16;   __VA_ARGS__; } break;              \
+    case HG_F32:  { using TIN = float;    __VA_ARGS__; } break;              \
+    case HG_F64:  { using TIN = double;   __VA_ARGS__; } break;              \
+    default: return HG_EDTYPE;                                               \
+    }
+
+#define HG_DISPATCH_FLOAT_OUT(dt, TOUT, ...)                                 \
+    switch (dt) {                                                            \
+    case HG_F16:  { using TOUT = _Float16; __VA_ARGS__; } break;             \
+    case HG_BF16: { using TOUT = __bf16;   __VA_ARGS__; } break;             \
+    case HG_F32:  { using TOUT = float;    __VA_ARGS__; } break;             \
+    case HG_F64:  { using TOUT = double;   __VA_ARGS__; } break;             \
+    default: return HG_EDTYPE;                                               \
+    }

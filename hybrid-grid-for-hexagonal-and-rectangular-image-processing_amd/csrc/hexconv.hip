@@ -1,0 +1,309 @@
+// hexconv.hip — gfx950 HexConv2d forward as a direct hex stencil.
+//
+// The reference (HexFrames.py:96-169) pads, expands the image to the
+// double-width "type1" raster (heximage_to_type1, :417-445), runs two strided
+// dense 3x5 F.conv2d (8 of 15 taps zero) and interleaves rows: about 7x the
+// compulsory traffic.  Here the type1 raster is never built.  With P the padded
+// image (H' = h+2p, W' = w+2p), o' = (off+p)%2 and L(y) = ((y&1)+o')&1, tap t =
+// (kernel row ii, cell m) of output (ro, q) reads
+//     P[s*ro + ii*d][s*q + dk_t(ro&1)],   dk_t(par) = (1 + par*s + t*d + 2dm - L(par*s+ii*d)) >> 1
+// (t = |ii-r+1|), and a column k >= W' is the type1 raster's structural zero.
+// See oracle/hg_oracle.c for the derivation against the reference lines.
+//
+// Workgroup = 256 threads, output tile 16 rows x 128 cols, thread t owns column
+// t%128 and 8 consecutive rows.  Per image and group, the tile's P footprint of
+// a chunk of input channels is staged into LDS (fp32/fp64, pad rules applied
+// once there), then each thread accumulates OCB output channels for its 8
+// samples; kernel weights are wave-uniform (scalar loads).
+#include <algorithm>
+#include <climits>
+
+#include "common.h"
+
+namespace hg {
+
+constexpr int CV_THREADS = 256;
+constexpr int CV_TC = 128;
+constexpr int CV_RPT = 8;
+constexpr int CV_TR = 16;
+constexpr int CV_MAXK = 128;          // taps: 3r^2-3r+1 <= 127 (r <= 7)
+constexpr int CV_LDS_BUDGET = 56 * 1024;
+
+struct ConvGeom {
+    int64_t B, C, O, h, w, ho, wo;
+    int r, s, p, d, groups, off, pad_mode;
+    int K, cg, og;
+    int ntx;          // tiles along output columns
+    int bc;           // images per workgroup
+    int cib;          // input channels staged per pass
+    int nPr, pitch;   // LDS footprint rows / pitch (elements)
+    int mink;         // min column tap offset over both parities
+    double pad_value;
+};
+
+__host__ __device__ inline int64_t pad_map(int64_t i, int64_t n, int mode) {
+    if (i >= 0 && i < n) return i;
+    switch (mode) {
+    case HG_PAD_REFLECT:
+        while (i < 0 || i >= n) { if (i < 0) i = -i; if (i >= n) i = 2 * (n - 1) - i; }
+        return i;
+    case HG_PAD_REPLICATE:
+        return i < 0 ? 0 : n - 1;
+    case HG_PAD_CIRCULAR:
+        return ((i % n) + n) % n;
+    default:
+        return -1;
+    }
+}
+
+// Tap table in kernel-flattening order (HexFrames.py:114-118).
+__host__ __device__ inline void tap_geom(int r, int s, int d, int op, int t, int* dy, int* dk0,
+                                         int* dk1) {
+    int n = 0;
+    for (int ii = 0; ii < 2 * r - 1; ++ii) {
+        int tt = ii - r + 1;
+        tt = tt < 0 ? -tt : tt;
+        const int ln = 2 * r - 1 - tt;
+        if (t < n + ln) {
+            const int m = t - n;
+            const int col = tt * d + 2 * d * m;
+            *dy = ii * d;
+            for (int par = 0; par < 2; ++par) {
+                const int y = par * s + ii * d;
+                const int L = ((y & 1) + op) & 1;
+                const int dk = (1 + par * s + col - L) >> 1;
+                if (par == 0) *dk0 = dk; else *dk1 = dk;
+            }
+            return;
+        }
+        n += ln;
+    }
+}
+
+template <typename Tin, typename Tout, typename A, int OCB, int KFIX>
+__global__ __launch_bounds__(CV_THREADS) void k_hexconv(const Tin* __restrict__ x,
+                                                        const A* __restrict__ kern,
+                                                        const A* __restrict__ bias,
+                                                        Tout* __restrict__ y, ConvGeom G) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int* tdy = reinterpret_cast<int*>(smem);
+    int* tdk = tdy + CV_MAXK;                 // [2][CV_MAXK]
+    A* tile = reinterpret_cast<A*>(smem + 3 * CV_MAXK * sizeof(int));
+
+    const int K = KFIX ? KFIX : G.K;
+    const int tid = threadIdx.x;
+    const int op = (G.off + G.p) & 1;
+    for (int t = tid; t < K; t += CV_THREADS) {
+        int dy, d0, d1;
+        tap_geom(G.r, G.s, G.d, op, t, &dy, &d0, &d1);
+        tdy[t] = dy;
+        tdk[t] = d0 - G.mink;
+        tdk[CV_MAXK + t] = d1 - G.mink;
+    }
+
+    const int tx = blockIdx.x % G.ntx, ty = blockIdx.x / G.ntx;
+    const int64_t r0 = (int64_t)ty * CV_TR, q0 = (int64_t)tx * CV_TC;
+    const int lq = tid & (CV_TC - 1);
+    const int lr0 = (tid / CV_TC) * CV_RPT;
+    const int64_t q = q0 + lq;
+    const int64_t Hp = G.h + 2 * G.p, Wp = G.w + 2 * G.p;
+    const int64_t pr0 = (int64_t)G.s * r0;                 // first staged P row
+    const int64_t pc0 = (int64_t)G.s * q0 + G.mink;        // first staged P col
+    const int chan = G.nPr * G.pitch;
+    const int64_t b0 = (int64_t)blockIdx.y * G.bc;
+    const int64_t b1 = std::min<int64_t>(b0 + G.bc, G.B);
+    const int64_t in_plane = G.h * G.w, out_plane = G.ho * G.wo;
+    const A padv = (A)G.pad_value;
+    __syncthreads();
+
+    for (int64_t b = b0; b < b1; ++b) {
+        for (int g = 0; g < G.groups; ++g) {
+            for (int oc0 = 0; oc0 < G.og; oc0 += OCB) {
+                A acc[CV_RPT][OCB];
+#pragma unroll
+                for (int j = 0; j < OCB; ++j) {
+                    const int o = g * G.og + oc0 + j;
+                    const A bv = (bias && oc0 + j < G.og) ? bias[o] : (A)0;
+#pragma unroll
+                    for (int k = 0; k < CV_RPT; ++k) acc[k][j] = bv;
+                }
+                for (int ci0 = 0; ci0 < G.cg; ci0 += G.cib) {
+                    const int nci = std::min(G.cib, G.cg - ci0);
+                    __syncthreads();
+                    // stage P footprint of nci channels
+                    const int per = G.nPr * G.pitch;
+                    for (int e = tid; e < nci * per; e += CV_THREADS) {
+                        const int cc = e / per;
+                        const int rem = e - cc * per;
+                        const int rr = rem / G.pitch;
+                        const int kk = rem - rr * G.pitch;
+                        const int64_t py = pr0 + rr, pk = pc0 + kk;
+                        A v = (A)0;
+                        if (py < Hp && pk >= 0 && pk < Wp) {
+                            const int64_t yi = pad_map(py - G.p, G.h, G.pad_mode);
+                            const int64_t xi = pad_map(pk - G.p, G.w, G.pad_mode);
+                            if (yi < 0 || xi < 0) v = padv;
+                            else {
+                                const Tin* xp = x + (b * G.C + g * G.cg + ci0 + cc) * in_plane;
+                                v = to_acc<A>(xp[yi * G.w + xi]);
+                            }
+                        }
+                        tile[e] = v;
+                    }
+                    __syncthreads();
+                    for (int cc = 0; cc < nci; ++cc) {
+                        const A* tc = tile + cc * chan;
+                        const A* kc = kern + ((int64_t)(g * G.og + oc0) * G.cg + ci0 + cc) * K;
+#pragma unroll 7
+                        for (int t = 0; t < K; ++t) {
+                            A wv[OCB];
+#pragma unroll
+                            for (int j = 0; j < OCB; ++j)
+                                wv[j] = (oc0 + j < G.og) ? kc[(int64_t)j * G.cg * K + t] : (A)0;
+                            const int dy = tdy[t];
+                            const int dke = tdk[t], dko = tdk[CV_MAXK + t];
+#pragma unroll
+                            for (int k = 0; k < CV_RPT; ++k) {
+                                const int lr = lr0 + k;
+                                const int dk = (k & 1) ? dko : dke;   // r0, lr0 even
+                                const A v = tc[(G.s * lr + dy) * G.pitch + G.s * lq + dk];
+#pragma unroll
+                                for (int j = 0; j < OCB; ++j) acc[k][j] += wv[j] * v;
+                            }
+                        }
+                    }
+                }
+                if (q < G.wo) {
+#pragma unroll
+                    for (int j = 0; j < OCB; ++j) {
+                        if (oc0 + j >= G.og) continue;
+                        Tout* yp = y + (b * G.O + g * G.og + oc0 + j) * out_plane;
+#pragma unroll
+                        for (int k = 0; k < CV_RPT; ++k) {
+                            const int64_t ro = r0 + lr0 + k;
+                            if (ro < G.ho) yp[ro * G.wo + q] = from_acc<Tout>(acc[k][j]);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+static int conv_out_shape(int64_t h, int64_t w, int r, int s, int p, int d, int64_t* ho,
+                          int64_t* wo) {
+    if (r < 1 || s < 1 || d < 1 || p < 0 || h < 0 || w < 0) return HG_EINVAL;
+    const int64_t kh = (int64_t)(2 * r - 2) * d + 1;
+    const int64_t kw = (int64_t)2 * d * (2 * r - 2) + 1;
+    const int64_t H = h + 2 * p, W = w + 2 * p;
+    if (H < kh || 2 * W - s < kw) return HG_ESHAPE;
+    *ho = (H - kh) / s + 1;
+    *wo = (2 * W - s - kw) / (2 * s) + 1;
+    return HG_OK;
+}
+
+template <typename Tin, typename Tout, typename A, int OCB, int KFIX>
+static int launch_conv(const void* x, const void* k, const void* b, void* y, ConvGeom G,
+                       hipStream_t st) {
+    const int64_t nty = (G.ho + CV_TR - 1) / CV_TR;
+    const int64_t tiles = (int64_t)G.ntx * nty;
+    int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>((2048 + tiles - 1) / tiles, G.B));
+    nchunk = std::min<int64_t>(nchunk, 65535);
+    G.bc = (int)((G.B + nchunk - 1) / nchunk);
+    const size_t shmem = 3 * CV_MAXK * sizeof(int) + (size_t)G.cib * G.nPr * G.pitch * sizeof(A);
+    dim3 grid((unsigned)tiles, (unsigned)((G.B + G.bc - 1) / G.bc));
+    hipLaunchKernelGGL((k_hexconv<Tin, Tout, A, OCB, KFIX>), grid, dim3(CV_THREADS), shmem, st,
+                       (const Tin*)x, (const A*)k, (const A*)b, (Tout*)y, G);
+    return launch_status();
+}
+
+template <typename Tin, typename Tout, typename A>
+static int conv_dispatch(const void* x, const void* k, const void* b, void* y,
+                         const ConvGeom& G, hipStream_t st) {
+    const bool k7 = G.K == 7;
+    if (G.og % 4 == 0 || G.og > 4) {
+        return k7 ? launch_conv<Tin, Tout, A, 4, 7>(x, k, b, y, G, st)
+                  : launch_conv<Tin, Tout, A, 4, 0>(x, k, b, y, G, st);
+    }
+    if (G.og == 3)
+        return k7 ? launch_conv<Tin, Tout, A, 3, 7>(x, k, b, y, G, st)
+                  : launch_conv<Tin, Tout, A, 3, 0>(x, k, b, y, G, st);
+    if (G.og == 2)
+        return k7 ? launch_conv<Tin, Tout, A, 2, 7>(x, k, b, y, G, st)
+                  : launch_conv<Tin, Tout, A, 2, 0>(x, k, b, y, G, st);
+    return k7 ? launch_conv<Tin, Tout, A, 1, 7>(x, k, b, y, G, st)
+              : launch_conv<Tin, Tout, A, 1, 0>(x, k, b, y, G, st);
+}
+
+}  // namespace hg
+
+extern "C" {
+
+int hg_hexconv2d_out_shape(int64_t h, int64_t w, int radius, int stride, int padding,
+                           int dilation, int64_t* ho, int64_t* wo) {
+    if (!ho || !wo) return HG_EINVAL;
+    return hg::conv_out_shape(h, w, radius, stride, padding, dilation, ho, wo);
+}
+
+int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, int x_dtype,
+                 int w_dtype, int y_dtype, int64_t batch, int64_t in_channels,
+                 int64_t out_channels, int64_t h, int64_t w, int radius, int stride,
+                 int padding, int dilation, int groups, int even_odd_offset, int pad_mode,
+                 double pad_value, void* stream) {
+    using namespace hg;
+    ConvGeom G;
+    int st = conv_out_shape(h, w, radius, stride, padding, dilation, &G.ho, &G.wo);
+    if (st) return st;
+    if (batch < 0 || in_channels < 1 || out_channels < 1 || groups < 1) return HG_EINVAL;
+    if (in_channels % groups || out_channels % groups) return HG_EINVAL;
+    if (pad_mode < HG_PAD_CONSTANT || pad_mode > HG_PAD_CIRCULAR) return HG_EINVAL;
+    if (pad_mode == HG_PAD_REFLECT && padding > 0 && (padding >= h || padding >= w))
+        return HG_ESHAPE;
+    if (pad_mode != HG_PAD_CONSTANT && padding > 0 && (h == 0 || w == 0)) return HG_ESHAPE;
+    if (pad_mode == HG_PAD_CIRCULAR && (padding > h || padding > w)) return HG_ESHAPE;
+    G.K = 3 * radius * radius - 3 * radius + 1;
+    if (G.K > CV_MAXK) return HG_EUNSUP;
+    if (batch == 0 || G.ho == 0 || G.wo == 0) return HG_OK;
+    if (!x || !kernel || !y) return HG_EINVAL;
+    if (w_dtype != HG_F32 && w_dtype != HG_F64) return HG_EDTYPE;
+    if (!dtype_is_float(y_dtype)) return HG_EDTYPE;
+    if (h * w >= INT_MAX / 2 || G.ho * G.wo >= INT_MAX / 2) return HG_ESHAPE;
+    G.B = batch; G.C = in_channels; G.O = out_channels; G.h = h; G.w = w;
+    G.r = radius; G.s = stride; G.p = padding; G.d = dilation; G.groups = groups;
+    G.off = even_odd_offset & 1; G.pad_mode = pad_mode; G.pad_value = pad_value;
+    G.cg = (int)(in_channels / groups);
+    G.og = (int)(out_channels / groups);
+    G.ntx = (int)((G.wo + CV_TC - 1) / CV_TC);
+    // column span of the taps over both row parities
+    const int op = (G.off + G.p) & 1;
+    int mink = INT_MAX, maxk = INT_MIN, maxdy = 0;
+    for (int t = 0; t < G.K; ++t) {
+        int dy, d0, d1;
+        tap_geom(radius, stride, dilation, op, t, &dy, &d0, &d1);
+        mink = std::min(mink, std::min(d0, d1));
+        maxk = std::max(maxk, std::max(d0, d1));
+        maxdy = std::max(maxdy, dy);
+    }
+    G.mink = mink;
+    G.nPr = stride * (CV_TR - 1) + maxdy + 1;
+    G.pitch = stride * (CV_TC - 1) + (maxk - mink) + 1;
+    G.pitch = (G.pitch + 3) & ~3;
+    const size_t esz = w_dtype == HG_F64 ? 8 : 4;
+    const size_t per = (size_t)G.nPr * G.pitch * esz;
+    if (per + 3 * CV_MAXK * sizeof(int) > (size_t)CV_LDS_BUDGET) return HG_EUNSUP;
+    G.cib = (int)std::min<size_t>((size_t)G.cg, (CV_LDS_BUDGET - 3 * CV_MAXK * sizeof(int)) / per);
+    G.bc = 1;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (w_dtype == HG_F64) {
+        HG_DISPATCH_IN(x_dtype, TIN, HG_DISPATCH_FLOAT_OUT(y_dtype, TOUT, {
+            return conv_dispatch<TIN, TOUT, double>(x, kernel, bias, y, G, s);
+        }));
+    } else {
+        HG_DISPATCH_IN(x_dtype, TIN, HG_DISPATCH_FLOAT_OUT(y_dtype, TOUT, {
+            return conv_dispatch<TIN, TOUT, float>(x, kernel, bias, y, G, s);
+        }));
+    }
+    return HG_EDTYPE;
+}
+
+}  // extern "C"

@@ -1,0 +1,163 @@
+// lattice.h — per-sample lattice geometry of the three resamplers.
+//
+// Everything here is evaluated in IEEE fp64 in the reference's NumPy order and
+// the library is built with -ffp-contract=off, so the integer maps (i_n, j_n,
+// the triangle flag, validity, nearest choice) and the fp64 coefficients are the
+// reference's bit for bit.  The functions run once per output sample per
+// workgroup and are reused for every plane the workgroup walks, so their fp64
+// cost is amortised over the whole batch.
+//
+// Citations: /root/reference/HyGrid/geometry_np.py, geometry_torch.py.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hg {
+
+// One numpy.linspace(start, stop, n) axis (geometry_np.py:415-422, :251-258).
+struct Axis {
+    double start, stop, delta, div, step;
+    int64_t n;
+};
+
+inline Axis make_axis(double start, double stop, int64_t n) {
+    Axis a;
+    a.start = start;
+    a.stop = stop;
+    a.n = n;
+    a.delta = stop - start;
+    a.div = n > 1 ? (double)(n - 1) : 0.0;
+    a.step = n > 1 ? a.delta / a.div : 0.0;
+    return a;
+}
+
+// numpy 2.2 linspace: y = k*step (or (k/div)*delta if step == 0); y += start;
+// y[-1] = stop.
+__host__ __device__ __forceinline__ double axis_at(const Axis& a, int64_t k) {
+    if (a.n > 1 && k == a.n - 1) return a.stop;
+    if (a.n > 1) {
+        double y = (a.step == 0.0) ? ((double)k / a.div) * a.delta : (double)k * a.step;
+        return y + a.start;
+    }
+    return (double)k * a.delta + a.start;
+}
+
+// Geometry of one resample call.
+struct Geom {
+    int64_t h, w, h1, w1;
+    Axis xs, ys;
+    double hh, ww;   // (double)h, (double)w
+};
+
+// rect -> hex: corners geometry_np.py:401-413.
+inline Geom make_r2h(int64_t h, int64_t w, int64_t h1, int64_t w1) {
+    Geom g;
+    g.h = h; g.w = w; g.h1 = h1; g.w1 = w1;
+    g.hh = (double)h; g.ww = (double)w;
+    g.xs = make_axis(-(g.hh / 2.0), g.hh / 2.0, h1);
+    g.ys = make_axis(-(g.ww / 2.0 + 0.5), g.ww / 2.0 + 0.5, w1);
+    return g;
+}
+
+// hex -> rect (margin .75, geometry_np.py:236-239) and hexresize (margin .5, :560-563).
+inline Geom make_tri(int64_t h, int64_t w, int64_t h1, int64_t w1, double margin) {
+    Geom g;
+    g.h = h; g.w = w; g.h1 = h1; g.w1 = w1;
+    g.hh = (double)h; g.ww = (double)w;
+    g.xs = make_axis(-(g.hh / 2.0 - 0.5), g.hh / 2.0 - 0.5, h1);
+    g.ys = make_axis(-((g.ww + 0.5) / 2.0 - margin), (g.ww + 0.5) / 2.0 - margin, w1);
+    return g;
+}
+
+// ---- rect -> hex sample (geometry_np.py:440-506) ----------------------------
+struct R2HSample {
+    int64_t i_n, j_n;
+    double i_f, j_f;
+    int valid;    // bit k: neighbour k+1 inside the raster (:465-476)
+    int argmin;   // nearest neighbour, first minimum (:499-506)
+};
+
+__host__ __device__ __forceinline__ R2HSample r2h_sample(const Geom& g, int64_t a, int64_t b) {
+    R2HSample s;
+    double x_ = axis_at(g.xs, a), y_ = axis_at(g.ys, b);
+    double i_ = x_ + (double)(g.h - 1) * 0.5;   // :440
+    double j_ = y_ + (double)(g.w - 1) * 0.5;   // :441
+    s.i_n = (int64_t)i_;                        // astype(int): toward zero
+    s.j_n = (int64_t)j_;
+    s.i_f = i_ - (double)(float)s.i_n;          // :448 i_n.astype(np.float32)
+    s.j_f = j_ - (double)(float)s.j_n;
+    s.valid = 0;
+    s.argmin = 0;
+    double best = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {               // 1=(i,j) 2=(i,j+1) 3=(i+1,j) 4=(i+1,j+1)
+        int64_t ii = s.i_n + (k >> 1), jj = s.j_n + (k & 1);
+        if (ii >= 0 && jj >= 0 && ii < g.h && jj < g.w) s.valid |= 1 << k;
+        double dx = x_ - (double)ii, dy = y_ - (double)jj;   // :499-502 (centred vs not)
+        double d = dx * dx + dy * dy;
+        if (k == 0 || d < best) { best = d; s.argmin = k; }
+    }
+    return s;
+}
+
+// ---- hex -> rect / hexresize sample (geometry_np.py:276-354) ----------------
+struct TriSample {
+    int64_t i_n, j_n;
+    int64_t r[3], c[3];   // p1, p2 (chosen by the flag), p3
+    int vk;               // validity bits of p1, p2, p3
+    int flag, valid, argmin;
+    double i_f, j_f, alpha, beta, gamma;
+};
+
+__host__ __device__ __forceinline__ TriSample tri_sample(const Geom& g, int64_t a, int64_t b) {
+    TriSample s;
+    const double hh = g.hh, ww = g.ww;
+    double x_ = axis_at(g.xs, a), y_ = axis_at(g.ys, b);
+    double i_ = x_ + (double)(g.h - 1) * 0.5;            // :276
+    double j_ = 0.5 * i_ + y_ + (ww - 0.5) * 0.5;        // :277
+    s.i_n = (int64_t)i_;
+    s.j_n = (int64_t)j_;
+    s.i_f = i_ - (double)(float)s.i_n;                   // :284-285
+    s.j_f = j_ - (double)(float)s.j_n;
+    int64_t s1 = (int64_t)((double)(s.i_n + 1) / 2.0);   // :289 true div, then trunc
+    int64_t s2 = (int64_t)((double)(s.i_n + 2) / 2.0);
+    int64_t ii[4] = {s.i_n, s.i_n + 1, s.i_n, s.i_n + 1};
+    int64_t jj[4] = {s.j_n - s1, s.j_n - s2, s.j_n + 1 - s1, s.j_n + 1 - s2};
+    s.flag = s.i_f > s.j_f;                              // :298
+    s.valid = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (ii[k] >= 0 && jj[k] >= 0 && ii[k] < g.h && jj[k] < g.w) s.valid |= 1 << k;
+    int k2 = s.flag ? 1 : 2;                             // :321-322
+    s.r[0] = ii[0]; s.c[0] = jj[0];
+    s.r[1] = ii[k2]; s.c[1] = jj[k2];
+    s.r[2] = ii[3]; s.c[2] = jj[3];
+    s.vk = (s.valid & 1) | (((s.valid >> k2) & 1) << 1) | (((s.valid >> 3) & 1) << 2);
+    // cartesian vertices :326-331
+    double fl = (double)s.flag, in = (double)s.i_n, jn = (double)s.j_n;
+    double p1_x = in - (hh - 1.0) / 2.0;
+    double p1_y = jn - in / 2.0 - (ww - 0.5) / 2.0;
+    double p2_x = (in + fl) - (hh - 1.0) / 2.0;
+    double p2_y = (jn + 1.0 - fl) - (in + fl) / 2.0 - (ww - 0.5) / 2.0;
+    double p3_x = (in + 1.0) - (hh - 1.0) / 2.0;
+    double p3_y = (jn + 1.0) - (in + 1.0) / 2.0 - (ww - 0.5) / 2.0;
+    // nearest (geometry_torch.py:336-341): first minimum of d1, d2, d3
+    double d1 = (x_ - p1_x) * (x_ - p1_x) + (y_ - p1_y) * (y_ - p1_y);
+    double d2 = (x_ - p2_x) * (x_ - p2_x) + (y_ - p2_y) * (y_ - p2_y);
+    double d3 = (x_ - p3_x) * (x_ - p3_x) + (y_ - p3_y) * (y_ - p3_y);
+    s.argmin = 0;
+    double best = d1;
+    if (d2 < best) { best = d2; s.argmin = 1; }
+    if (d3 < best) { s.argmin = 2; }
+    // barycentric weights :348-353
+    double S1 = 0.5 * fabs((x_ - p2_x) * (y_ - p3_y) - (y_ - p2_y) * (x_ - p3_x));
+    double S2 = 0.5 * fabs((x_ - p1_x) * (y_ - p3_y) - (y_ - p1_y) * (x_ - p3_x));
+    double S3 = 0.5 * fabs((x_ - p1_x) * (y_ - p2_y) - (y_ - p1_y) * (x_ - p2_x));
+    double S = S1 + S2 + S3;
+    s.alpha = S1 / S;
+    s.beta = S2 / S;
+    s.gamma = S3 / S;
+    return s;
+}
+
+}  // namespace hg

@@ -1,0 +1,112 @@
+/*
+ * hygrid.h — C ABI of libhygrid_hip.so, the MI355X (gfx950) hex<->rect lattice
+ * resampling and hex-convolution hot path.
+ *
+ * Contract (all entry points):
+ *   - Plain pointers to DEVICE memory, caller-allocated and contiguous
+ *     (planar, row-major: (planes, h, w) for the resamplers, (B, C, H, W) for
+ *     the convolution).  The library never allocates, frees or retains caller
+ *     memory and holds no global mutable state: every call is reentrant.
+ *   - Work is enqueued on `stream` (a hipStream_t; NULL = the null stream) with
+ *     no host synchronisation inside, so calls may be captured in a hipGraph.
+ *   - Return value: HG_OK (0) on success, a negative HG_E* for argument / shape
+ *     / dtype errors (nothing is launched), or a positive hipError_t.
+ *     hg_strerror() renders either kind.
+ *
+ * Each entry point cites the reference interface it replaces
+ * (paths under Tesla-Albert/Hybrid-Grid-for-Hexagonal-and-Rectangular-Image-Processing).
+ * The reference has no native code and no FFI of its own; its Python surface is
+ * mirrored on top of this ABI by the HyGrid package.
+ */
+#ifndef HYGRID_H
+#define HYGRID_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HG_ABI_VERSION 1
+
+/* Element types (dtype codes). */
+enum hg_dtype {
+    HG_U8 = 0, HG_I8 = 1, HG_U16 = 2, HG_I16 = 3, HG_I32 = 4, HG_I64 = 5,
+    HG_F16 = 6, HG_BF16 = 7, HG_F32 = 8, HG_F64 = 9
+};
+
+/* Interpolation codes.  HG_LINEAR is 'bilinear' for rect->hex
+ * (geometry_np.py:359-363) and 'linear' (3-vertex triangle) for hex->rect and
+ * hexresize (geometry_np.py:192-197, :672). */
+enum hg_interp { HG_NEAREST = 0, HG_LINEAR = 1 };
+
+/* Padding modes of HexConv2d (HexFrames.py:13-21 -> torch.nn.functional.pad). */
+enum hg_pad_mode { HG_PAD_CONSTANT = 0, HG_PAD_REFLECT = 1, HG_PAD_REPLICATE = 2,
+                   HG_PAD_CIRCULAR = 3 };
+
+/* Lattice-map operation codes for hg_lattice_maps. */
+enum hg_op { HG_OP_RECT_TO_HEX = 0, HG_OP_HEX_TO_RECT = 1, HG_OP_HEXRESIZE = 2 };
+
+/* Status codes. */
+#define HG_OK 0
+#define HG_EINVAL (-1)   /* bad argument (null pointer, non-positive size, bad enum) */
+#define HG_EDTYPE (-2)   /* unsupported dtype or dtype combination */
+#define HG_ESHAPE (-3)   /* input too small for the operator / size overflow */
+#define HG_EUNSUP (-4)   /* combination not implemented */
+
+int hg_abi_version(void);
+const char* hg_strerror(int status);
+
+/* rect -> hex lattice resample.
+ * Replaces geometry_np.rect_to_hex_resample(rect_image, hex_dsize, interpolation,
+ * offset) (HyGrid/geometry_np.py:358-519) for `planes` images at once.
+ * src: (planes, h, w) of src_dtype; dst: (planes, h1, w1) of dst_dtype.
+ * HG_NEAREST copies the chosen source element (dst_dtype must equal src_dtype);
+ * HG_LINEAR needs a floating dst_dtype (F64 reproduces the reference's fp64
+ * output bit for bit).  `offset` is dead in the reference (:358), so absent here. */
+int hg_rect_to_hex(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t planes,
+                   int64_t h, int64_t w, int64_t h1, int64_t w1, int interp, void* stream);
+
+/* hex -> rect lattice resample.
+ * Replaces geometry_np.hex_to_rect_resample (HyGrid/geometry_np.py:191-356,
+ * 'linear') and geometry_torch.hex_to_square_resample
+ * (HyGrid/geometry_torch.py:191-358, 'nearest' rule :335-347). */
+int hg_hex_to_rect(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t planes,
+                   int64_t h, int64_t w, int64_t h1, int64_t w1, int interp, void* stream);
+
+/* hex -> hex resize.  Replaces geometry_np.hexresize (HyGrid/geometry_np.py:520-681). */
+int hg_hexresize(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t planes,
+                 int64_t h, int64_t w, int64_t h1, int64_t w1, int interp, void* stream);
+
+/* Integer lattice maps (and fp64 coefficients) of one resample, for parity tests.
+ * imaps: int32 [5][h1][w1] = i_n, j_n, up_down_flag, valid bitmask (bit k-1 =
+ *        valid_indices_k), nearest argmin — the locals of the reference function
+ *        (geometry_np.py:444-476 / :280-315, geometry_torch.py:341).
+ * fmaps: float64 [5][h1][w1] = i_f, j_f, alpha, beta, gamma (rect->hex fills the
+ *        first two).  Either may be NULL. */
+int hg_lattice_maps(int op, int64_t h, int64_t w, int64_t h1, int64_t w1, int32_t* imaps,
+                    double* fmaps, void* stream);
+
+/* Output size of HexConv2d (HexFrames.py:127-169): ho = floor((H'-k_h)/s)+1,
+ * wo = floor((2W'-s-k_w)/(2s))+1 with H' = h+2p, W' = w+2p, k_h = (2r-2)d+1,
+ * k_w = 2d(2r-2)+1.  Host-only; returns HG_ESHAPE when the reference would fail. */
+int hg_hexconv2d_out_shape(int64_t h, int64_t w, int radius, int stride, int padding,
+                           int dilation, int64_t* ho, int64_t* wo);
+
+/* HexConv2d forward.  Replaces HexFrames.HexConv2d.forward (HexFrames.py:96-169)
+ * including pad (:13-21) and heximage_to_type1 (:417-445), which are folded into
+ * index arithmetic: no type1 image is materialised.
+ * x: (B, C, h, w) of x_dtype; kernel: (O, C/groups, K) with K = 3r^2-3r+1 (the
+ * reference parameter `kernel` [O, C/g, 1, K], :74) of w_dtype (F32 or F64);
+ * bias: (O,) of w_dtype or NULL; y: (B, O, ho, wo) of y_dtype.
+ * Accumulates in w_dtype, as the reference (`input.to(self.kernel.dtype)`, :107). */
+int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, int x_dtype,
+                 int w_dtype, int y_dtype, int64_t batch, int64_t in_channels,
+                 int64_t out_channels, int64_t h, int64_t w, int radius, int stride,
+                 int padding, int dilation, int groups, int even_odd_offset, int pad_mode,
+                 double pad_value, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYGRID_H */
