@@ -53,6 +53,10 @@ def parse():
                     help="max images in the CPU-baseline sample (~10 s; 0 disables it)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
     ap.add_argument("--no-gather", action="store_true", help="skip the timed output gather")
+    ap.add_argument("--unfused", action="store_true",
+                    help="time the three operators (r2h, HexConv2d, h2r) instead of the fused kernel")
+    ap.add_argument("--no-compare", action="store_true",
+                    help="skip the secondary (unfused) measurement in the fused run")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-kernel HBM bytes from rocprofv3 PMC passes (optional)")
     return ap.parse_args()
@@ -95,6 +99,7 @@ def main():
 
     from HyGrid import ops
     from HyGrid.HexFrames import HexConv2d
+    from HyGrid.pipeline import rect_hex_conv_rect
 
     B, C, H, W = args.batch, args.channels, args.height, args.width
     bf16 = torch.bfloat16
@@ -104,10 +109,7 @@ def main():
     conv = HexConv2d(C, C, 0, 2, padding=1, groups=1, bias=True).to(dev)
     conv.out_dtype = bf16
 
-    stages = ("rect_to_hex", "hexconv2d", "hex_to_rect")
-    ev = []
-
-    def step(record):
+    def run_unfused(record, ev):
         if record:
             e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             e[0].record()
@@ -123,33 +125,52 @@ def main():
             ev.append(e)
         return y
 
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            y = step(False)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            y = step(True)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
+    def run_fused(record, ev):
+        if record:
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            e[0].record()
+        y = rect_hex_conv_rect(x, conv, (H, W), (H, W), out_dtype=bf16)
+        if record:
+            e[1].record()
+            ev.append(e)
+        return y
 
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    def measure(fn, steps, warmup):
+        """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
+        ev = []
+        with torch.no_grad():
+            for _ in range(warmup):
+                y = fn(False, ev)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                y = fn(True, ev)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t1 = time.perf_counter()
+        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        n = len(ev[0]) - 1
+        # per-kernel times from HIP events recorded on the launch stream
+        stage_ms = [sum(e[i].elapsed_time(e[i + 1]) for e in ev) / len(ev) for i in range(n)]
+        return y, float(el.item()), stage_ms
+
+    img_bytes = B * C * H * W * 2          # one bf16 batch tensor
+    if args.unfused:
+        stages = ("rect_to_hex", "hexconv2d", "hex_to_rect")
+        y, elapsed, sms = measure(run_unfused, args.steps, args.warmup)
+    else:
+        stages = ("pipeline_r2h_conv_h2r",)
+        y, elapsed, sms = measure(run_fused, args.steps, args.warmup)
+    stage_ms = dict(zip(stages, sms))
     ms_per_step = elapsed / args.steps * 1e3
     mpix = world * B * H * W * args.steps / elapsed / 1e6
-
-    # per-stage kernel times (HIP events on the launch stream, timed region only)
-    stage_ms = {s: sum(e[i].elapsed_time(e[i + 1]) for e in ev) / len(ev)
-                for i, s in enumerate(stages)}
-    elem = 2  # bf16 bytes
-    alg_bytes = {s: 2 * B * C * H * W * elem for s in stages}   # read once + write once
+    alg_bytes = {s: 2 * img_bytes for s in stages}   # each kernel: read once + write once
     kernels = {s: {"ms": round(stage_ms[s], 4), "alg_GB": round(alg_bytes[s] / 1e9, 4),
                    "GB_per_s": round(alg_bytes[s] / (stage_ms[s] * 1e-3) / 1e9, 1)}
                for s in stages}
@@ -167,6 +188,19 @@ def main():
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "alg_bytes_per_launch": alg_bytes[dom]}
+
+    compare = None
+    if not args.unfused and not args.no_compare:
+        # the three-operator chain on the same data, reported beside `value` (never as it)
+        steps_u = max(2, args.steps // 2)
+        _, el_u, sms_u = measure(run_unfused, steps_u, 1)
+        ks = ("rect_to_hex", "hexconv2d", "hex_to_rect")
+        compare = {"path": "rect_to_hex -> HexConv2d -> hex_to_rect (3 kernels, bf16 between)",
+                   "value": round(world * B * H * W * steps_u / el_u / 1e6, 1),
+                   "ms_per_step": round(el_u / steps_u * 1e3, 4),
+                   "kernels": {k: {"ms": round(m, 4),
+                                   "GB_per_s": round(2 * img_bytes / (m * 1e-3) / 1e9, 1)}
+                               for k, m in zip(ks, sms_u)}}
 
     # checksums over RCCL (not timed), and the full-output gather on its own
     from HyGrid.dist import gather_checksums, gather_to_root, image_checksums
@@ -207,15 +241,15 @@ def main():
             "metric": metric, "value": round(mpix, 1), "unit": "Mpix/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-            "data": f"synthetic U[0,1) bf16 rasters generated on device, seed 2+rank; "
-                    f"HexConv2d weights torch.manual_seed(3) + reference init",
+            "data": "synthetic U[0,1) bf16 rasters generated on device, seed 2+rank; "
+                    "HexConv2d weights torch.manual_seed(3) + reference init",
             "config": {"workload": "config3: 4K RGB batch=128/GPU, rect->hex bilinear -> "
                                    "HexConv2d(3,3,off=0,r=2,pad=1) -> hex->rect linear",
                        "batch_per_gpu": B, "global_batch": B * world, "channels": C,
                        "height": H, "width": W, "parallelism": f"dp{world}",
-                       "fused": False},
+                       "fused": not args.unfused},
             "kernels": kernels, "roofline": roofline, "cpu_baseline": cpu,
-            "gather": gather, "checksum": checksum,
+            "unfused": compare, "gather": gather, "checksum": checksum,
             "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)

@@ -129,3 +129,37 @@ def hexconv2d(x, kernel, bias, even_odd_offset, radius, stride=1, padding=0, dil
 def hexconv2d_backward(gy, x, kernel, bias, cfg, need_x, need_k, need_b):
     """Gradients of hexconv2d."""
     raise NotImplementedError("HexConv2d backward kernels are not built yet")
+
+
+HG_EUNSUP = -4
+
+
+def pipeline_r2h_conv_h2r(x, kernel, bias, hex_size=None, rect_size=None, padding=1, groups=1,
+                          even_odd_offset=0, padding_value=0.0, out_dtype=None):
+    """Fused rect -> hex (bilinear) -> HexConv2d (radius 2) -> hex -> rect (linear).
+
+    Returns None when the fused kernel does not cover the geometry / dtypes (the
+    caller then runs the three operators); raises on argument errors.
+    """
+    _abi.require_device(x)
+    while x.dim() < 4:
+        x = x.unsqueeze(0)
+    x = x.contiguous()
+    B, C, h, w = (int(s) for s in x.shape)
+    h1, w1 = (h, w) if hex_size is None else (int(hex_size[0]), int(hex_size[1]))
+    ho, wo = hexconv2d_out_shape(h1, w1, 2, 1, padding, 1)
+    h2, w2 = (ho, wo) if rect_size is None else (int(rect_size[0]), int(rect_size[1]))
+    k = kernel.detach().float().reshape(kernel.shape[0], -1).contiguous()
+    O = int(k.shape[0])
+    b = bias.detach().float().contiguous() if bias is not None else None
+    if out_dtype is None:
+        out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
+    y = torch.empty((B, O, h2, w2), dtype=out_dtype, device=x.device)
+    st = _abi.lib().hg_pipeline_r2h_conv_h2r(
+        _abi.ptr(x), _abi.ptr(k), _abi.ptr(b), _abi.ptr(y), _abi.dtype_code(x.dtype),
+        _abi.dtype_code(out_dtype), B, C, O, h, w, h1, w1, h2, w2, int(padding), int(groups),
+        int(even_odd_offset), float(padding_value), _abi.stream_of(x))
+    if st in (HG_EUNSUP, -2):
+        return None
+    _abi.check(st, "hg_pipeline_r2h_conv_h2r")
+    return y

@@ -190,6 +190,43 @@ __global__ __launch_bounds__(CV_THREADS) void k_hexconv(const Tin* __restrict__ 
     }
 }
 
+// Direct-gather fallback (footprint larger than the LDS budget: large radius or
+// stride).  One thread per output sample, taps read straight from global memory.
+template <typename Tin, typename Tout, typename A>
+__global__ __launch_bounds__(256) void k_hexconv_direct(const Tin* __restrict__ x,
+                                                        const A* __restrict__ kern,
+                                                        const A* __restrict__ bias,
+                                                        Tout* __restrict__ y, ConvGeom G) {
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = G.B * G.O * G.ho * G.wo;
+    if (idx >= total) return;
+    const int64_t q = idx % G.wo;
+    const int64_t ro = (idx / G.wo) % G.ho;
+    const int64_t o = (idx / (G.wo * G.ho)) % G.O;
+    const int64_t b = idx / (G.wo * G.ho * G.O);
+    const int g = (int)(o / G.og);
+    const int op = (G.off + G.p) & 1;
+    const int64_t Wp = G.w + 2 * G.p;
+    A acc = bias ? bias[o] : (A)0;
+    for (int t = 0; t < G.K; ++t) {
+        int dy, d0, d1;
+        tap_geom(G.r, G.s, G.d, op, t, &dy, &d0, &d1);
+        const int64_t py = (int64_t)G.s * ro + dy;
+        const int64_t pk = (int64_t)G.s * q + ((ro & 1) ? d1 : d0);
+        if (pk >= Wp) continue;                          // type1 structural zero
+        const int64_t yi = pad_map(py - G.p, G.h, G.pad_mode);
+        const int64_t xi = pad_map(pk - G.p, G.w, G.pad_mode);
+        for (int ci = 0; ci < G.cg; ++ci) {
+            const A wv = kern[(o * G.cg + ci) * G.K + t];
+            A v;
+            if (yi < 0 || xi < 0) v = (A)G.pad_value;
+            else v = to_acc<A>(x[((b * G.C + g * G.cg + ci) * G.h + yi) * G.w + xi]);
+            acc += wv * v;
+        }
+    }
+    y[idx] = from_acc<Tout>(acc);
+}
+
 static int conv_out_shape(int64_t h, int64_t w, int r, int s, int p, int d, int64_t* ho,
                           int64_t* wo) {
     if (r < 1 || s < 1 || d < 1 || p < 0 || h < 0 || w < 0) return HG_EINVAL;
@@ -220,6 +257,12 @@ static int launch_conv(const void* x, const void* k, const void* b, void* y, Con
 template <typename Tin, typename Tout, typename A>
 static int conv_dispatch(const void* x, const void* k, const void* b, void* y,
                          const ConvGeom& G, hipStream_t st) {
+    if (G.cib == 0) {
+        const int64_t total = G.B * G.O * G.ho * G.wo;
+        hipLaunchKernelGGL((k_hexconv_direct<Tin, Tout, A>), dim3((unsigned)((total + 255) / 256)),
+                           dim3(256), 0, st, (const Tin*)x, (const A*)k, (const A*)b, (Tout*)y, G);
+        return launch_status();
+    }
     const bool k7 = G.K == 7;
     if (G.og % 4 == 0 || G.og > 4) {
         return k7 ? launch_conv<Tin, Tout, A, 4, 7>(x, k, b, y, G, st)
@@ -290,8 +333,11 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
     G.pitch = (G.pitch + 3) & ~3;
     const size_t esz = w_dtype == HG_F64 ? 8 : 4;
     const size_t per = (size_t)G.nPr * G.pitch * esz;
-    if (per + 3 * CV_MAXK * sizeof(int) > (size_t)CV_LDS_BUDGET) return HG_EUNSUP;
-    G.cib = (int)std::min<size_t>((size_t)G.cg, (CV_LDS_BUDGET - 3 * CV_MAXK * sizeof(int)) / per);
+    if (per + 3 * CV_MAXK * sizeof(int) > (size_t)CV_LDS_BUDGET)
+        G.cib = 0;   // footprint too large for LDS: direct-gather kernel
+    else
+        G.cib = (int)std::min<size_t>((size_t)G.cg,
+                                      (CV_LDS_BUDGET - 3 * CV_MAXK * sizeof(int)) / per);
     G.bc = 1;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (w_dtype == HG_F64) {

@@ -106,6 +106,23 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
                  int padding, int dilation, int groups, int even_odd_offset, int pad_mode,
                  double pad_value, void* stream);
 
+/* Fused rect -> hex -> HexConv2d -> hex -> rect pass over a batch.
+ * Replaces the chain rect_to_hex_resample(x, (h1,w1), 'bilinear')
+ * (geometry_np.py:358-519) -> HexConv2d(C, O, even_odd_offset, 2, stride=1,
+ * padding, dilation=1, groups, padding_mode='constant', padding_value)
+ * (HexFrames.py:22-169) -> hex_to_rect_resample(., (h2,w2), 'linear')
+ * (geometry_np.py:191-356), as a user script runs it (SURVEY.md §3 B+C).
+ * x: (B, C, h, w); kernel: (O, C/groups, 7) float32; bias: (O,) float32 or NULL;
+ * y: (B, O, h2, w2).  Intermediates stay on chip in fp32 (one read of x, one
+ * write of y).  C, O in {1, 3}; x_dtype in {U8, F16, BF16, F32}, y_dtype in
+ * {F16 (f16 in only), BF16, F32}.  Returns HG_EUNSUP when the geometry is not
+ * near-identity (then run the three operators instead). */
+int hg_pipeline_r2h_conv_h2r(const void* x, const float* kernel, const float* bias, void* y,
+                             int x_dtype, int y_dtype, int64_t batch, int64_t channels,
+                             int64_t out_channels, int64_t h, int64_t w, int64_t h1, int64_t w1,
+                             int64_t h2, int64_t w2, int padding, int groups,
+                             int even_odd_offset, double pad_value, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

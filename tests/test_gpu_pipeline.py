@@ -1,0 +1,92 @@
+"""GPU parity of the fused rect->hex->HexConv2d->hex->rect kernel
+(hg_pipeline_r2h_conv_h2r) against the CPU oracle chain, and against the
+unfused HIP chain.  fp32: rtol 1e-5 (atol 1e-5*max|ref|); bf16 output: one bf16
+rounding (2^-8)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from HyGrid import ops  # noqa: E402
+from HyGrid.HexFrames import HexConv2d  # noqa: E402
+from HyGrid.pipeline import rect_hex_conv_rect  # noqa: E402
+
+DEV = torch.device("cuda:0")
+
+
+def close(y, ref, rtol):
+    y = np.asarray(y, np.float64)
+    scale = max(np.abs(ref).max(), 1e-30)
+    np.testing.assert_allclose(y, ref, rtol=rtol, atol=rtol * scale)
+
+
+def oracle_chain(x, conv, hex_size, rect_size):
+    h = O.rect_to_hex(x.double().cpu().numpy(), hex_size, 1)
+    b = conv.bias.detach().cpu().numpy() if conv.bias is not None else None
+    c = O.hexconv2d(h, conv.kernel.detach().cpu().numpy(), b, int(conv.even_odd_offset), 2,
+                    padding=conv.pad, groups=conv.groups, padding_value=conv.padding_value)
+    return O.hex_to_rect(c, rect_size, 1)
+
+
+CASES = [
+    # (B, C, H, W, hex_size, rect_size, off, pad, groups, pad_value)
+    (2, 3, 48, 80, None, None, 0, 1, 1, 0.0),
+    (1, 3, 37, 53, None, None, 1, 1, 1, 0.0),
+    (2, 3, 64, 150, None, None, 0, 1, 3, 0.0),
+    (1, 3, 40, 70, None, None, 1, 0, 1, 0.0),
+    (1, 3, 40, 70, None, None, 0, 2, 1, 0.3),
+    (3, 1, 33, 200, None, None, 0, 1, 1, 0.0),
+    (1, 3, 70, 130, (71, 131), (70, 130), 0, 1, 1, 0.0),
+    (1, 3, 9, 7, None, None, 0, 1, 1, 0.0),
+    (1, 3, 270, 480, None, None, 0, 1, 1, 0.0),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_fused_vs_oracle_fp32(case):
+    B, C, H, W, hs, rs, off, pad, g, pv = case
+    torch.manual_seed(3)
+    conv = HexConv2d(C, C, off, 2, padding=pad, groups=g, bias=True, padding_value=pv).to(DEV)
+    x = torch.rand((B, C, H, W), device=DEV)
+    with torch.no_grad():
+        y = ops.pipeline_r2h_conv_h2r(x, conv.kernel, conv.bias, hs, rs, pad, g, off, pv,
+                                      torch.float32)
+    assert y is not None, "geometry should be fusable"
+    hs_ = hs or (H, W)
+    ho, wo = ops.hexconv2d_out_shape(hs_[0], hs_[1], 2, 1, pad, 1)
+    ref = oracle_chain(x, conv, hs_, rs or (ho, wo))
+    close(y.cpu().numpy(), ref, 1e-5)
+
+
+def test_fused_4k_bf16_matches_oracle_and_unfused():
+    """BASELINE config-3 geometry at full size (2 images)."""
+    torch.manual_seed(3)
+    conv = HexConv2d(3, 3, 0, 2, padding=1, bias=True).to(DEV)
+    gen = torch.Generator(device=DEV).manual_seed(2)
+    x = torch.rand((2, 3, 2160, 3840), generator=gen, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        y = rect_hex_conv_rect(x, conv)
+        y32 = rect_hex_conv_rect(x, conv, out_dtype=torch.float32)
+        unf = rect_hex_conv_rect(x, conv, out_dtype=torch.float32, fused=False)
+    assert y.dtype == torch.bfloat16 and y.shape == x.shape
+    ref = oracle_chain(x[1:2], conv, (2160, 3840), (2160, 3840))[0]
+    close(y32[1].cpu().numpy(), ref, 1e-5)
+    close(y[1].float().cpu().numpy(), ref, 2 ** -8)
+    close(unf.cpu().numpy(), y32.cpu().numpy().astype(np.float64), 1e-5)
+
+
+def test_non_identity_geometry_falls_back():
+    torch.manual_seed(3)
+    conv = HexConv2d(3, 3, 0, 2, padding=1, bias=True).to(DEV)
+    x = torch.rand((1, 3, 64, 96), device=DEV)
+    with torch.no_grad():
+        assert ops.pipeline_r2h_conv_h2r(x, conv.kernel, conv.bias, (32, 48), (64, 96)) is None
+        y = rect_hex_conv_rect(x, conv, (32, 48), (64, 96))
+    ref = oracle_chain(x, conv, (32, 48), (64, 96))
+    close(y.cpu().numpy(), ref, 1e-5)

@@ -1,0 +1,43 @@
+"""Profiling driver: runs one operator of the hot path a few times on a synthetic
+4K bf16 batch so that rocprofv3 (kernel trace / PMC passes) can attribute it.
+
+usage: python tools/prof_pipeline.py [fused|r2h|conv|h2r] [batch] [iters]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hybrid-grid-for-hexagonal-and-rectangular-image-processing_amd")]
+
+import torch  # noqa: E402
+
+from HyGrid import ops  # noqa: E402
+from HyGrid.HexFrames import HexConv2d  # noqa: E402
+from HyGrid.pipeline import rect_hex_conv_rect  # noqa: E402
+
+
+def main():
+    what = sys.argv[1] if len(sys.argv) > 1 else "fused"
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    iters = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    dev = torch.device("cuda:0")
+    H, W = 2160, 3840
+    x = torch.rand((B, 3, H, W), device=dev, dtype=torch.bfloat16)
+    torch.manual_seed(3)
+    conv = HexConv2d(3, 3, 0, 2, padding=1, bias=True).to(dev)
+    conv.out_dtype = torch.bfloat16
+    with torch.no_grad():
+        for _ in range(iters):
+            if what == "fused":
+                rect_hex_conv_rect(x, conv, out_dtype=torch.bfloat16)
+            elif what == "r2h":
+                ops.rect_to_hex(x, (H, W), out_dtype=torch.bfloat16)
+            elif what == "conv":
+                conv(x)
+            elif what == "h2r":
+                ops.hex_to_rect(x, (H, W), out_dtype=torch.bfloat16)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
