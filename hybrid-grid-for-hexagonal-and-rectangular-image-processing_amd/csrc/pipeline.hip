@@ -399,6 +399,19 @@ __device__ __forceinline__ float2v pk_fma(float2v a, float2v b, float2v c) {
     return __builtin_elementwise_fma(a, b, c);
 }
 
+template <typename T>
+__device__ __forceinline__ void buf_store(T v, __amdgpu_buffer_rsrc_t rs, unsigned voff,
+                                          unsigned soff) {
+    if constexpr (sizeof(T) == 2)
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, v), rs, voff, soff, 0);
+    else if constexpr (sizeof(T) == 4)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, voff, soff, 0);
+    else {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rs, voff, soff, 0);
+    }
+}
+
 // Raw buffer load of one element: SGPR descriptor + VGPR byte offset + SGPR byte
 // offset, so a row fetch costs no per-lane address arithmetic.
 template <typename T>
@@ -480,6 +493,13 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
                                                    (int)(cstride * (int64_t)sizeof(Tin)),
                                                    0x00020000);
     const unsigned lbyte = lcol * (unsigned)sizeof(Tin);
+    __amdgpu_buffer_rsrc_t yrs[O];      // one buffer descriptor per output channel plane
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+        yrs[o] = __builtin_amdgcn_make_buffer_rsrc((void*)(yb + o * ostride), (short)0,
+                                                   (int)(ostride * (int64_t)sizeof(Tout)),
+                                                   0x00020000);
+    const unsigned obytecol = ocol * (unsigned)sizeof(Tout);
 #pragma unroll
     for (int k = 0; k < NSET; ++k) { FI[k] = GI[k] = 0.f; XOK[k] = 0; }
 
@@ -502,13 +522,20 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
                    (r >= 0 && r < F.h1 ? 4 : 0);
     };
 
-    float U[3][NS][C];                  // u row r in slot r % 3, lane shifts -1 .. DKMAX-1
+    // u row r in slot r % 3 at lane shifts -1 .. DKMAX-1.  For three channels the
+    // values are held as a (c0, c1) pair + c2, the operand shape of the packed conv.
+    constexpr bool PK = C == 3 && O == 3 && G == 1;
+    constexpr int CS = PK ? 1 : C;      // scalar channels kept in U
+    float2v UP[3][NS];                  // (c0, c1)         (PK only)
+    float U[3][NS][CS];                 // c2 (PK) or all channels
 #pragma unroll
-    for (int c = 0; c < C; ++c)
+    for (int s3 = 0; s3 < 3; ++s3)
 #pragma unroll
-        for (int s3 = 0; s3 < 3; ++s3)
+        for (int d = 0; d < NS; ++d) {
+            UP[s3][d] = float2v{0.f, 0.f};
 #pragma unroll
-            for (int d = 0; d < NS; ++d) U[s3][d][c] = 0.f;
+            for (int c = 0; c < CS; ++c) U[s3][d][c] = 0.f;
+        }
 
     // u row from register set SET into slot SL
     auto compute_u = [&](auto SLc, auto SETc) {
@@ -527,33 +554,43 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
             const float u = fmaf(wr[0], vm, fmaf(wr[1], v, fmaf(wr[2], vp, wr[3] * vq)));
             uv[c] = (uok && col_in_w1) ? u : colpad;                 // pad rows / cols
         }
+        float sh[NS][C];                // lane shifts -1 .. DKMAX-1 of every channel
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            U[SL][1][c] = uv[c];
-            U[SL][0][c] = dpp_prev(uv[c]);
-            U[SL][2][c] = dpp_next(uv[c]);
-            if constexpr (NS == 4) U[SL][3][c] = dpp_next(U[SL][2][c]);
+            sh[1][c] = uv[c];
+            sh[0][c] = dpp_prev(uv[c]);
+            sh[2][c] = dpp_next(uv[c]);
+            if constexpr (NS == 4) sh[3][c] = dpp_next(sh[2][c]);
+        }
+#pragma unroll
+        for (int d = 0; d < NS; ++d) {
+            if constexpr (PK) {
+                UP[SL][d] = float2v{sh[d][0], sh[d][1]};
+                U[SL][d][0] = sh[d][2];
+            } else {
+#pragma unroll
+                for (int c = 0; c < C; ++c) U[SL][d][c] = sh[d][c];
+            }
         }
     };
 
-    // kernel weights, loaded once into VGPRs; for C = O = 3, groups 1 they are held
-    // as pairs for packed FMA: (w[0][c][t], w[1][c][t]) and (w[2][0][t], w[2][1][t])
-    constexpr bool PK = C == 3 && O == 3 && G == 1;
-    float2v w01[PK ? 21 : 1], w2p[PK ? 7 : 1];
-    float w2s[PK ? 7 : 1], wk[PK ? 1 : O * CG * 7], bs[O];
-    // an opaque per-lane zero makes the weight loads vector loads: the weights are
-    // meant to live in VGPRs (SGPRs are needed for the row / descriptor state)
+    // kernel weights, loaded once into VGPRs.  For C = O = 3, groups 1: per output o
+    // and tap t the pair (w[o][0][t], w[o][1][t]) for the packed (c0, c1) FMA, and
+    // w[o][2][t] for c2.  An opaque per-lane zero makes these vector loads (the
+    // SGPRs are needed for the row / descriptor state).
     int vz = 0;
     asm volatile("" : "+v"(vz));
     const float* kv = kern + vz;
+    float2v wp2[PK ? O * 7 : 1];
+    float wk[PK ? O * 7 : O * CG * 7], bs[O];
     if constexpr (PK) {
 #pragma unroll
-        for (int t = 0; t < 7; ++t) {
+        for (int o = 0; o < O; ++o)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) w01[t * 3 + c] = float2v{kv[c * 7 + t], kv[(3 + c) * 7 + t]};
-            w2p[t] = float2v{kv[6 * 7 + t], kv[7 * 7 + t]};
-            w2s[t] = kv[8 * 7 + t];
-        }
+            for (int t = 0; t < 7; ++t) {
+                wp2[o * 7 + t] = float2v{kv[(o * 3 + 0) * 7 + t], kv[(o * 3 + 1) * 7 + t]};
+                wk[o * 7 + t] = kv[(o * 3 + 2) * 7 + t];
+            }
     } else {
 #pragma unroll
         for (int i = 0; i < O * CG * 7; ++i) wk[i] = kv[i];
@@ -568,25 +605,20 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
         constexpr int SLT[3] = {(PH + 2) % 3, PH % 3, (PH + 1) % 3};   // rows a2-1, a2, a2+1
         const bool zok = a2 < F.ho && col_in_wo;
         if constexpr (PK) {
-            // (o0, o1) packed over every tap and channel; o2 packed over (c0, c1)
-            float2v a01 = {bs[0], bs[1]};
-            float2v a2p = {bs[2], 0.f};
-            float a2s = 0.f;
+            // per output: packed FMA over the (c0, c1) pair + scalar FMA for c2
 #pragma unroll
-            for (int t = 0; t < 7; ++t) {
-                const int sl = SLT[tap_ii(t)];
-                const int dk = tap_dk(t, PAR, OP);
+            for (int o = 0; o < 3; ++o) {
+                float2v ap = {bs[o], 0.f};
+                float as = 0.f;
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const float u = U[sl][dk][c];
-                    a01 = pk_fma(w01[t * 3 + c], float2v{u, u}, a01);
+                for (int t = 0; t < 7; ++t) {
+                    const int sl = SLT[tap_ii(t)];
+                    const int dk = tap_dk(t, PAR, OP);
+                    ap = pk_fma(wp2[o * 7 + t], UP[sl][dk], ap);
+                    as = fmaf(wk[o * 7 + t], U[sl][dk][0], as);
                 }
-                a2p = pk_fma(w2p[t], float2v{U[sl][dk][0], U[sl][dk][1]}, a2p);
-                a2s = fmaf(w2s[t], U[sl][dk][2], a2s);
+                z[o] = zok ? (ap.x + ap.y) + as : 0.f;
             }
-            z[0] = zok ? a01.x : 0.f;
-            z[1] = zok ? a01.y : 0.f;
-            z[2] = zok ? (a2p.x + a2p.y) + a2s : 0.f;
         } else {
 #pragma unroll
             for (int o = 0; o < O; ++o) {
@@ -612,15 +644,15 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
                   std::integral_constant<int, (PH + 1) % NSET>{});
         float z[O];
         conv_row(PHc, a2, z);
+        const unsigned obyte = (unsigned)(a2 * F.w2) * (unsigned)sizeof(Tout);
 #pragma unroll
         for (int o = 0; o < O; ++o) {
-            Tout* orow = yb + (o * ostride + (int64_t)a2 * F.w2);   // uniform row pointer
             float out;
             if constexpr ((PH & 1) == 0)   // even row: 0.75 z[b] + 0.25 z[b+1]
                 out = fmaf(0.75f, z[o], 0.25f * dpp_next(z[o]));
             else                           // odd row: 0.25 z[b-1] + 0.75 z[b]
                 out = fmaf(0.25f, dpp_prev(z[o]), 0.75f * z[o]);
-            if (own) orow[ocol] = from_acc<Tout>(out);
+            if (own) buf_store<Tout>(from_acc<Tout>(out), yrs[o], obytecol, obyte);
         }
     };
 
