@@ -278,6 +278,10 @@ static int conv_dispatch(const void* x, const void* k, const void* b, void* y,
               : launch_conv<Tin, Tout, A, 1, 0>(x, k, b, y, G, st);
 }
 
+int launch_conv_stream(const void* x, const float* k, const float* b, void* y, int x_dtype,
+                       int y_dtype, int64_t B, int C, int O, int64_t h, int64_t w, int p,
+                       int groups, int off, double pad_value, hipStream_t st);   // conv_stream.hip
+
 }  // namespace hg
 
 extern "C" {
@@ -311,6 +315,15 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
     if (w_dtype != HG_F32 && w_dtype != HG_F64) return HG_EDTYPE;
     if (!dtype_is_float(y_dtype)) return HG_EDTYPE;
     if (h * w >= INT_MAX / 2 || G.ho * G.wo >= INT_MAX / 2) return HG_ESHAPE;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (radius == 2 && stride == 1 && dilation == 1 && pad_mode == HG_PAD_CONSTANT &&
+        w_dtype == HG_F32 && in_channels <= 3 && out_channels <= 3) {
+        // register-streaming fast path (conv_stream.hip); EUNSUP -> generic kernel
+        st = launch_conv_stream(x, (const float*)kernel, (const float*)bias, y, x_dtype, y_dtype,
+                                batch, (int)in_channels, (int)out_channels, h, w, padding,
+                                groups, even_odd_offset & 1, pad_value, s);
+        if (st != HG_EUNSUP) return st;
+    }
     G.B = batch; G.C = in_channels; G.O = out_channels; G.h = h; G.w = w;
     G.r = radius; G.s = stride; G.p = padding; G.d = dilation; G.groups = groups;
     G.off = even_odd_offset & 1; G.pad_mode = pad_mode; G.pad_value = pad_value;
@@ -339,7 +352,6 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
         G.cib = (int)std::min<size_t>((size_t)G.cg,
                                       (CV_LDS_BUDGET - 3 * CV_MAXK * sizeof(int)) / per);
     G.bc = 1;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (w_dtype == HG_F64) {
         HG_DISPATCH_IN(x_dtype, TIN, HG_DISPATCH_FLOAT_OUT(y_dtype, TOUT, {
             return conv_dispatch<TIN, TOUT, double>(x, kernel, bias, y, G, s);

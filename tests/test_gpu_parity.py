@@ -251,3 +251,30 @@ def test_hexconv_param_space_vs_oracle(cfg, mode):
         ref = O.hexconv2d(x.numpy(), k.numpy(), b.numpy(), off, cfg["r"], cfg["s"], cfg["p"],
                           cfg["d"], cfg["g"], mode, 0.25)
         close(y.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("cg", [(3, 3, 1), (3, 3, 3), (1, 1, 1)])
+@pytest.mark.parametrize("p", [0, 1, 2])
+def test_hexconv_stream_path_vs_oracle(cg, p):
+    """radius 2 / stride 1 / constant padding: the register-streaming kernel
+    (conv_stream.hip).  Ragged widths (window halos), heights across row bands
+    (126 rows) and the 6-row unroll, both row-parity offsets, nonzero padding value."""
+    c, o, g = cg
+    torch.manual_seed(17 + p)
+    k = torch.randn((o, c // g, 7))
+    b = torch.randn(o)
+    for (h, w) in [(3, 3), (7, 61), (127, 130), (253, 200), (5, 1)]:
+        if w + 2 * p - 2 < 1 or h + 2 * p - 2 < 1:
+            continue
+        x = torch.rand((2, c, h, w), dtype=torch.float32)
+        for off in (0, 1):
+            ref = O.hexconv2d(x.double().numpy(), k.numpy(), b.numpy(), off, 2, 1, p, 1, g,
+                              "constant", 0.375)
+            for dt in (torch.float32, torch.bfloat16, torch.float16):
+                xd = x.to(dt)
+                ref_d = ref if dt == torch.float32 else O.hexconv2d(
+                    xd.double().numpy(), k.numpy(), b.numpy(), off, 2, 1, p, 1, g, "constant", 0.375)
+                y = ops.hexconv2d(xd.to(DEV), k.to(DEV), b.to(DEV), off, 2, 1, p, 1, g,
+                                  "constant", 0.375)
+                assert y.shape == ref_d.shape
+                close(y.cpu().numpy(), ref_d)
