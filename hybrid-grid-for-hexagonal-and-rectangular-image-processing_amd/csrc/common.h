@@ -49,6 +49,23 @@ inline int hip_status(hipError_t e) { return e == hipSuccess ? HG_OK : (int)e; }
 
 inline int launch_status() { return hip_status(hipGetLastError()); }
 
+// XCD-aware block order.  Blocks are dealt to the 8 XCDs round-robin (bid % 8 labels
+// the blocks that share an XCD and its private L2); this bijection hands each XCD a
+// contiguous run of logical blocks, so neighbouring windows / tiles, whose halos
+// share 128-B lines, are fetched into the same L2 instead of into two
+// (cdna_hip_programming.md T1, bijective form for nwg % 8 != 0).  Speed only: any
+// placement is correct.
+__device__ __forceinline__ unsigned xcd_swizzle(unsigned bid, unsigned nwg) {
+    const unsigned q = nwg >> 3, r = nwg & 7u, x = bid & 7u;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+// The same for a 2-D grid in dispatch (x-fastest) order: returns the logical (x, y).
+__device__ __forceinline__ void xcd_swizzle2(unsigned* bx, unsigned* by) {
+    const unsigned s = xcd_swizzle(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+    *bx = s % gridDim.x;
+    *by = s / gridDim.x;
+}
+
 }  // namespace hg
 
 // Instantiate `FN<Tin, Tout>(args...)` for every supported (in, out) dtype pair.

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void k_hexconv_stream(const Tin* __restrict__ 
     constexpr int PD = 2, NSET = 3;
     constexpr bool PK = C == 3 && O == 3 && G == 1;
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wave = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int win = (int)(wave % F.nwin);
     const int64_t rest = wave / F.nwin;
     const int band = (int)(rest % F.nband);

@@ -101,7 +101,9 @@ __global__ __launch_bounds__(CV_THREADS) void k_hexconv(const Tin* __restrict__ 
         tdk[CV_MAXK + t] = d1 - G.mink;
     }
 
-    const int tx = blockIdx.x % G.ntx, ty = blockIdx.x / G.ntx;
+    unsigned bx, by;
+    xcd_swizzle2(&bx, &by);
+    const int tx = (int)bx % G.ntx, ty = (int)bx / G.ntx;
     const int64_t r0 = (int64_t)ty * CV_TR, q0 = (int64_t)tx * CV_TC;
     const int lq = tid & (CV_TC - 1);
     const int lr0 = (tid / CV_TC) * CV_RPT;
@@ -110,7 +112,7 @@ __global__ __launch_bounds__(CV_THREADS) void k_hexconv(const Tin* __restrict__ 
     const int64_t pr0 = (int64_t)G.s * r0;                 // first staged P row
     const int64_t pc0 = (int64_t)G.s * q0 + G.mink;        // first staged P col
     const int chan = G.nPr * G.pitch;
-    const int64_t b0 = (int64_t)blockIdx.y * G.bc;
+    const int64_t b0 = (int64_t)by * G.bc;
     const int64_t b1 = std::min<int64_t>(b0 + G.bc, G.B);
     const int64_t in_plane = G.h * G.w, out_plane = G.ho * G.wo;
     const A padv = (A)G.pad_value;

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline(const Tin* __restrict__
     const int lane = threadIdx.x & 63;
     // wave index made provably wave-uniform: everything derived from it (image, band,
     // window, row bounds, base pointers, buffer descriptors) then lives in SGPRs
-    const int64_t wave = (int64_t)blockIdx.x * (PL_THREADS / 64) +
+    const int64_t wave = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (PL_THREADS / 64) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int win = (int)(wave % F.nwin);
     const int64_t rest = wave / F.nwin;
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
     const int lane = threadIdx.x & 63;
     // wave index made provably wave-uniform: everything derived from it (image, band,
     // window, row bounds, base pointers, buffer descriptors) then lives in SGPRs
-    const int64_t wave = (int64_t)blockIdx.x * (PL_THREADS / 64) +
+    const int64_t wave = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (PL_THREADS / 64) +
                          __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int win = (int)(wave % F.nwin);
     const int64_t rest = wave / F.nwin;

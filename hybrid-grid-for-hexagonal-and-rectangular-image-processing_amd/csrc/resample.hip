@@ -173,10 +173,12 @@ __global__ __launch_bounds__(RS_THREADS, 2) void k_resample_lds(const Tin* __res
 
     const Geom& g = L.g;
     const int tid = threadIdx.x;
-    const int tx = blockIdx.x % L.ntx, ty = blockIdx.x / L.ntx;
+    unsigned bx, by;
+    xcd_swizzle2(&bx, &by);
+    const int tx = (int)bx % L.ntx, ty = (int)bx / L.ntx;
     const int64_t b = (int64_t)tx * RS_TC + (tid & (RS_TC - 1));
     const int64_t a0 = (int64_t)ty * RS_TR + (tid / RS_TC) * RS_RPT;
-    const int64_t p0 = (int64_t)blockIdx.y * L.pc;
+    const int64_t p0 = (int64_t)by * L.pc;
     const int64_t p1 = p0 + L.pc < L.planes ? p0 + L.pc : L.planes;
     const int64_t in_plane = g.h * g.w, out_plane = g.h1 * g.w1;
     const bool bact = b < g.w1;
@@ -269,10 +271,12 @@ __global__ __launch_bounds__(RS_THREADS, 2) void k_resample_direct(const Tin* __
                                                                   LaunchGeom L) {
     const Geom& g = L.g;
     const int tid = threadIdx.x;
-    const int tx = blockIdx.x % L.ntx, ty = blockIdx.x / L.ntx;
+    unsigned bx, by;
+    xcd_swizzle2(&bx, &by);
+    const int tx = (int)bx % L.ntx, ty = (int)bx / L.ntx;
     const int64_t b = (int64_t)tx * RS_TC + (tid & (RS_TC - 1));
     const int64_t a0 = (int64_t)ty * RS_TR + (tid / RS_TC) * RS_RPT;
-    const int64_t p0 = (int64_t)blockIdx.y * L.pc;
+    const int64_t p0 = (int64_t)by * L.pc;
     const int64_t p1 = p0 + L.pc < L.planes ? p0 + L.pc : L.planes;
     const int64_t in_plane = g.h * g.w, out_plane = g.h1 * g.w1;
     if (b >= g.w1) return;
@@ -330,10 +334,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_resample_nearest(const E* __rest
                                                                  LaunchGeom L) {
     const Geom& g = L.g;
     const int tid = threadIdx.x;
-    const int tx = blockIdx.x % L.ntx, ty = blockIdx.x / L.ntx;
+    unsigned bx, by;
+    xcd_swizzle2(&bx, &by);
+    const int tx = (int)bx % L.ntx, ty = (int)bx / L.ntx;
     const int64_t b = (int64_t)tx * RS_TC + (tid & (RS_TC - 1));
     const int64_t a0 = (int64_t)ty * RS_TR + (tid / RS_TC) * RS_RPT;
-    const int64_t p0 = (int64_t)blockIdx.y * L.pc;
+    const int64_t p0 = (int64_t)by * L.pc;
     const int64_t p1 = p0 + L.pc < L.planes ? p0 + L.pc : L.planes;
     if (b >= g.w1) return;
     int off[RS_RPT];

@@ -1,7 +1,10 @@
 """Profiling driver: runs one operator of the hot path a few times on a synthetic
 4K bf16 batch so that rocprofv3 (kernel trace / PMC passes) can attribute it.
 
-usage: python tools/prof_pipeline.py [fused|r2h|conv|h2r] [batch] [iters]
+usage: python tools/prof_pipeline.py [fused|r2h|conv|h2r|r2h_nearest|copy] [batch] [iters]
+
+`copy` (torch bf16 clone) and `r2h_nearest` (one read + one write of every element) are
+the known-byte calibration runs for the FETCH_SIZE/WRITE_SIZE counters.
 """
 import os
 import sys
@@ -36,6 +39,12 @@ def main():
                 conv(x)
             elif what == "h2r":
                 ops.hex_to_rect(x, (H, W), out_dtype=torch.bfloat16)
+            elif what == "r2h_nearest":
+                ops.rect_to_hex(x, (H, W), interp=0)
+            elif what == "copy":
+                x.clone()
+            else:
+                raise SystemExit(f"unknown stage {what!r}")
     torch.cuda.synchronize()
 
 
