@@ -56,13 +56,13 @@ __host__ __device__ constexpr int tap_dk(int t, int par, int op) {
 // (GFX9 DPP wave_shl:1 / wave_shr:1, full VALU rate, no LDS round trip) build a
 // small window of shifted copies, and each lane selects its offset from it.
 __device__ __forceinline__ float lane_get(float v, int src) { return __shfl(v, src, 64); }
-__device__ __forceinline__ float dpp_next(float v) {   // result[l] = v[l+1]
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-        0, __builtin_bit_cast(int, v), 0x130 /*wave_shl:1*/, 0xf, 0xf, false));
+__device__ __forceinline__ float dpp_next(float v) {   // result[l] = v[l+1], 0 past lane 63
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+        __builtin_bit_cast(int, v), 0x130 /*wave_shl:1*/, 0xf, 0xf, true));
 }
-__device__ __forceinline__ float dpp_prev(float v) {   // result[l] = v[l-1]
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
-        0, __builtin_bit_cast(int, v), 0x138 /*wave_shr:1*/, 0xf, 0xf, false));
+__device__ __forceinline__ float dpp_prev(float v) {   // result[l] = v[l-1], 0 before lane 0
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+        __builtin_bit_cast(int, v), 0x138 /*wave_shr:1*/, 0xf, 0xf, true));
 }
 // s[k - LO] = v[l + k] for k in [LO, HI]
 template <int LO, int HI>
@@ -428,6 +428,9 @@ __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t rs, unsigned voff, 
     }
 }
 
+// Rows of the per-wave r2h row table: u rows [a2_begin - 1, a2_begin + RB + 2].
+constexpr int PL_LUT = 136;
+
 template <typename Tin, typename Tout, int C, int O, int G, int OP>
 __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict__ x,
                                                            const float* __restrict__ kern,
@@ -436,11 +439,15 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
     constexpr int CG = C / G, OG = O / G;
     constexpr int DKMAX = OP ? 2 : 3;          // stencil shifts dk in [0, DKMAX], lanes dk-1
     constexpr int NS = DKMAX + 1;
+    // per-wave r2h row table: {byte offset of row in, of row in+1, fi, 1-fi} with the
+    // weight of an out-of-range rect row folded to 0 (geometry_np.py:465-486)
+    __shared__ uint4 lut_all[PL_THREADS / 64][PL_LUT];
     const int lane = threadIdx.x & 63;
+    const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4* lut = lut_all[wslot];
     // wave index made provably wave-uniform: everything derived from it (image, band,
     // window, row bounds, base pointers, buffer descriptors) then lives in SGPRs
-    const int64_t wave = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (PL_THREADS / 64) +
-                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t wave = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (PL_THREADS / 64) + wslot;
     const int win = (int)(wave % F.nwin);
     const int64_t rest = wave / F.nwin;
     const int band = (int)(rest % F.nband);
@@ -450,8 +457,28 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
     const int col = W0 + lane;
     const int a2_begin = band * F.RB;                 // F.RB % 6 == 0
     const int a2_end = min(a2_begin + F.RB, F.h2);
+    const int ubase = a2_begin - 1;                   // u row of lut[0]
 
-    // r2h column weights over the lane window [-1, 2]: u = sum_k wr[k+1] * v[lane+k]
+    // row table: lane l fills entries l, l+64, l+128 (fp64 lattice math, :440-449)
+    for (int e = lane; e < PL_LUT; e += 64) {
+        const int r = min(max(ubase + e, 0), F.h1 - 1);
+        const double i_ = axis_at(F.r2h.xs, r) + (double)(F.h - 1) * 0.5;   // :440
+        const int in = (int)i_;
+        const double f = i_ - (double)(float)in;
+        const bool ok0 = in >= 0 && in < F.h, ok1 = in + 1 >= 0 && in + 1 < F.h;
+        uint4 t;
+        t.x = (unsigned)(min(max(in, 0), F.h - 1) * F.w) * (unsigned)sizeof(Tin);
+        t.y = (unsigned)(min(max(in + 1, 0), F.h - 1) * F.w) * (unsigned)sizeof(Tin);
+        t.z = __builtin_bit_cast(unsigned, ok1 ? (float)f : 0.f);
+        t.w = __builtin_bit_cast(unsigned, ok0 ? (float)(1.0 - f) : 0.f);
+        lut[e] = t;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): own-wave LDS writes visible
+    __builtin_amdgcn_wave_barrier();
+
+    // r2h column weights over the lane window [-1, 2]: u = sum_k wr[k+1] * v[lane+k].
+    // A tap on a rect column outside [0, w) reads 0 in the reference: its weight is 0
+    // here, so v may hold anything finite there (the loads are column-clamped).
     float wr[4] = {0.f, 0.f, 0.f, 0.f};
     if (col >= 0 && col < F.w1) {
         const double j_ = axis_at(F.r2h.ys, col) + (double)(F.w - 1) * 0.5;   // :441
@@ -460,11 +487,11 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
         const int kl = (int)(jn - col);
 #pragma unroll
         for (int k = -1; k <= 2; ++k) {
-            if (k == kl) wr[k + 1] = (float)(1.0 - jf);   // weight of t1 = v[jn]
-            if (k == kl + 1) wr[k + 1] = (float)jf;       // weight of t2 = v[jn+1]
+            const bool in_w = col + k >= 0 && col + k < F.w;
+            if (k == kl && in_w) wr[k + 1] = (float)(1.0 - jf);   // weight of t1 = v[jn]
+            if (k == kl + 1 && in_w) wr[k + 1] = (float)jf;       // weight of t2 = v[jn+1]
         }
     }
-    const bool col_in_w = col >= 0 && col < F.w;
     const bool col_in_w1 = col >= 0 && col < F.w1;
     const float colpad = col >= F.w1 + 1 ? 0.f : F.padv;           // structural 0 / pad
     const bool col_in_wo = col >= 0 && col < F.wo;
@@ -477,15 +504,12 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
     const int64_t cstride = (int64_t)F.h * F.w;
     const int64_t ostride = (int64_t)F.h2 * F.w2;
 
-    // Input path, branch-free: at phase P the rect rows (in, in+1) of u row r+PD are
-    // loaded into register set (P + PD) % 6 and consumed PD steps later.  Row indices
-    // are clamped (the loads never sit in a branch, so the waitcnt pass keeps them in
-    // flight across steps) and out-of-range rows / columns are zeroed at use.
+    // Input path, branch-free: the rect rows (in, in+1) of u row r are loaded PD steps
+    // before use into register set r % 3; row offsets and weights come from the table.
     constexpr int PD = 2;               // u rows loaded ahead
     constexpr int NSET = 3;             // register sets, keyed by row % 3 (3 | 6)
     Tin X[NSET][2][C];                  // [set][row in / in+1][channel]
     float FI[NSET], GI[NSET];           // row weights of the set's u row (uniform)
-    int XOK[NSET];                      // bit0: row in valid, bit1: row in+1 valid, bit2: u row valid
     __amdgpu_buffer_rsrc_t xrs[C];      // one buffer descriptor per input channel plane
 #pragma unroll
     for (int c = 0; c < C; ++c)
@@ -501,25 +525,19 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
                                                    0x00020000);
     const unsigned obytecol = ocol * (unsigned)sizeof(Tout);
 #pragma unroll
-    for (int k = 0; k < NSET; ++k) { FI[k] = GI[k] = 0.f; XOK[k] = 0; }
+    for (int k = 0; k < NSET; ++k) FI[k] = GI[k] = 0.f;
 
     auto issue = [&](auto SETc, int r) {       // loads for u row r into set SET
         constexpr int SET = decltype(SETc)::value;
-        const int rc = min(max(r, 0), F.h1 - 1);
-        const double i_ = axis_at(F.r2h.xs, rc) + (double)(F.h - 1) * 0.5;    // :440
-        const int in = uniform((int)i_);
-        const double f = i_ - (double)(float)in;
-        FI[SET] = __builtin_bit_cast(float, uniform(__builtin_bit_cast(int, (float)f)));
-        GI[SET] = __builtin_bit_cast(float, uniform(__builtin_bit_cast(int, (float)(1.0 - f))));
-        const unsigned r0 = (unsigned)(min(max(in, 0), F.h - 1) * F.w) * (unsigned)sizeof(Tin);
-        const unsigned r1 = (unsigned)(min(max(in + 1, 0), F.h - 1) * F.w) * (unsigned)sizeof(Tin);
+        const uint4 t = lut[r - ubase];          // uniform address: LDS broadcast
+        const unsigned r0 = uniform((int)t.x), r1 = uniform((int)t.y);
+        FI[SET] = __builtin_bit_cast(float, uniform((int)t.z));
+        GI[SET] = __builtin_bit_cast(float, uniform((int)t.w));
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             X[SET][0][c] = buf_load<Tin>(xrs[c], lbyte, r0);
             X[SET][1][c] = buf_load<Tin>(xrs[c], lbyte, r1);
         }
-        XOK[SET] = (in >= 0 && in < F.h ? 1 : 0) | (in + 1 >= 0 && in + 1 < F.h ? 2 : 0) |
-                   (r >= 0 && r < F.h1 ? 4 : 0);
     };
 
     // u row r in slot r % 3 at lane shifts -1 .. DKMAX-1.  For three channels the
@@ -537,22 +555,20 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
             for (int c = 0; c < CS; ++c) U[s3][d][c] = 0.f;
         }
 
-    // u row from register set SET into slot SL
-    auto compute_u = [&](auto SLc, auto SETc) {
+    // u row r from register set SET into slot SL
+    auto compute_u = [&](auto SLc, auto SETc, int r) {
         constexpr int SL = decltype(SLc)::value;
         constexpr int SET = decltype(SETc)::value;
-        const int ok = XOK[SET];
-        const bool ok0 = (ok & 1) && col_in_w, ok1 = (ok & 2) && col_in_w;
-        const bool uok = (ok & 4) != 0;
+        const bool uok = (r >= 0 && r < F.h1) && col_in_w1;
         float uv[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            const float x0 = ok0 ? to_acc<float>(X[SET][0][c]) : 0.f;
-            const float x1 = ok1 ? to_acc<float>(X[SET][1][c]) : 0.f;
+            const float x0 = to_acc<float>(X[SET][0][c]);
+            const float x1 = to_acc<float>(X[SET][1][c]);
             const float v = fmaf(FI[SET], x1, GI[SET] * x0);         // t = fi*p3 + (1-fi)*p1
-            const float vm = dpp_prev(v), vp = dpp_next(v), vq = dpp_next(vp);
-            const float u = fmaf(wr[0], vm, fmaf(wr[1], v, fmaf(wr[2], vp, wr[3] * vq)));
-            uv[c] = (uok && col_in_w1) ? u : colpad;                 // pad rows / cols
+            const float vp = dpp_next(v), vq = dpp_next(vp);
+            const float u = fmaf(wr[0], dpp_prev(v), fmaf(wr[1], v, fmaf(wr[2], vp, wr[3] * vq)));
+            uv[c] = uok ? u : colpad;                                 // pad rows / cols
         }
         float sh[NS][C];                // lane shifts -1 .. DKMAX-1 of every channel
 #pragma unroll
@@ -636,15 +652,15 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
         }
     };
 
-    // one output row a2 (phase PH = a2 % 6): u row a2+1 lives in set (PH + 1) % 6
+    // one output row a2 (phase PH = a2 % 6): u row a2+1 lives in set (PH + 1) % 3
     auto step = [&](auto PHc, int a2) {
         constexpr int PH = decltype(PHc)::value;
         issue(std::integral_constant<int, (PH + 1 + PD) % NSET>{}, a2 + 1 + PD);
         compute_u(std::integral_constant<int, (PH + 1) % 3>{},
-                  std::integral_constant<int, (PH + 1) % NSET>{});
+                  std::integral_constant<int, (PH + 1) % NSET>{}, a2 + 1);
         float z[O];
         conv_row(PHc, a2, z);
-        const unsigned obyte = (unsigned)(a2 * F.w2) * (unsigned)sizeof(Tout);
+        const unsigned obyte = (unsigned)uniform(a2 * F.w2) * (unsigned)sizeof(Tout);
 #pragma unroll
         for (int o = 0; o < O; ++o) {
             float out;
@@ -661,9 +677,9 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
     issue(std::integral_constant<int, 2>{}, a2_begin - 1);
     issue(std::integral_constant<int, 0>{}, a2_begin);
     issue(std::integral_constant<int, 1>{}, a2_begin + 1);
-    compute_u(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
+    compute_u(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, a2_begin - 1);
     issue(std::integral_constant<int, 2>{}, a2_begin + 2);
-    compute_u(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    compute_u(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, a2_begin);
     for (int base = a2_begin; base < a2_end; base += 6) {
         step(std::integral_constant<int, 0>{}, base);
         if (base + 1 >= a2_end) break;
