@@ -428,14 +428,22 @@ __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t rs, unsigned voff, 
     }
 }
 
-// Rows of the per-wave r2h row table: u rows [a2_begin - 1, a2_begin + RB + 2].
+// Tuning knobs of the static kernel (compile-time; tools/build_variant.sh sweeps them).
+#ifndef PL_S_PD
+#define PL_S_PD 2            // u rows whose rect rows are loaded ahead
+#endif
+#ifndef PL_S_WPE
+#define PL_S_WPE 0           // min waves per SIMD requested from the register allocator
+#endif
+// Rows of the per-wave r2h row table: u rows [a2_begin - 1, a2_begin + RB + PD].
 constexpr int PL_LUT = 136;
 
-template <typename Tin, typename Tout, int C, int O, int G, int OP>
-__global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict__ x,
-                                                           const float* __restrict__ kern,
-                                                           const float* __restrict__ bias,
-                                                           Tout* __restrict__ y, PipeGeom F) {
+// R3: every live r2h tap lies in the lane window [-1, 1] (jn - q in {-1, 0} wherever
+// a tap is in range, e.g. same-size resamples); otherwise the window is [-1, 2].
+template <typename Tin, typename Tout, int C, int O, int G, int OP, bool R3>
+__global__ __launch_bounds__(PL_THREADS) __attribute__((amdgpu_waves_per_eu(PL_S_WPE ? PL_S_WPE : 1)))
+void k_pipeline_s(const Tin* __restrict__ x, const float* __restrict__ kern,
+                  const float* __restrict__ bias, Tout* __restrict__ y, PipeGeom F) {
     constexpr int CG = C / G, OG = O / G;
     constexpr int DKMAX = OP ? 2 : 3;          // stencil shifts dk in [0, DKMAX], lanes dk-1
     constexpr int NS = DKMAX + 1;
@@ -476,24 +484,30 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): own-wave LDS writes visible
     __builtin_amdgcn_wave_barrier();
 
-    // r2h column weights over the lane window [-1, 2]: u = sum_k wr[k+1] * v[lane+k].
+    // r2h column weights over the lane window [-1, NR-2]: u = sum_k wr[k+1] * v[lane+k].
     // A tap on a rect column outside [0, w) reads 0 in the reference: its weight is 0
     // here, so v may hold anything finite there (the loads are column-clamped).
-    float wr[4] = {0.f, 0.f, 0.f, 0.f};
+    constexpr int NR = R3 ? 3 : 4;
+    float wr[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) wr[k] = 0.f;
     if (col >= 0 && col < F.w1) {
         const double j_ = axis_at(F.r2h.ys, col) + (double)(F.w - 1) * 0.5;   // :441
         const int64_t jn = (int64_t)j_;
         const double jf = j_ - (double)(float)jn;
         const int kl = (int)(jn - col);
 #pragma unroll
-        for (int k = -1; k <= 2; ++k) {
+        for (int k = -1; k <= NR - 2; ++k) {
             const bool in_w = col + k >= 0 && col + k < F.w;
             if (k == kl && in_w) wr[k + 1] = (float)(1.0 - jf);   // weight of t1 = v[jn]
             if (k == kl + 1 && in_w) wr[k + 1] = (float)jf;       // weight of t2 = v[jn+1]
         }
     }
     const bool col_in_w1 = col >= 0 && col < F.w1;
-    const float colpad = col >= F.w1 + 1 ? 0.f : F.padv;           // structural 0 / pad
+    // padding cells hold padv; u columns >= w1 + 1 are the type1 raster's structural
+    // zeros, read only by OP == 0 outputs (for OP == 1 they reach only z columns >= wo,
+    // which are zeroed), so for OP == 1 colpad stays wave-uniform
+    const float colpad = (OP == 0 && col >= F.w1 + 1) ? 0.f : F.padv;
     const bool col_in_wo = col >= 0 && col < F.wo;
     const bool own = lane >= F.HL && lane < F.HL + F.nown && col >= 0 && col < F.w2;
     const unsigned lcol = (unsigned)min(max(col, 0), F.w - 1);   // clamped lane offset
@@ -505,10 +519,16 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
     const int64_t ostride = (int64_t)F.h2 * F.w2;
 
     // Input path, branch-free: the rect rows (in, in+1) of u row r are loaded PD steps
-    // before use into register set r % 3; row offsets and weights come from the table.
-    constexpr int PD = 2;               // u rows loaded ahead
-    constexpr int NSET = 3;             // register sets, keyed by row % 3 (3 | 6)
-    Tin X[NSET][2][C];                  // [set][row in / in+1][channel]
+    // before use into register set (r - a2_begin) mod NSET; row offsets and weights
+    // come from the table.
+    constexpr int PD = PL_S_PD;         // u rows loaded ahead
+    static_assert(PD >= 2 && PD <= 4, "row table holds RB + 2 + PD <= PL_LUT rows");
+    constexpr int NSET = PD + 1 <= 3 ? 3 : 6;   // register sets keyed by row % NSET (NSET | 6)
+    // [set][channel] rows (in, in+1); 16-bit types share one VGPR (d16 / d16_hi loads)
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    constexpr bool X16 = sizeof(Tin) == 2;
+    using XT = typename std::conditional<X16, u16x2, Tin[2]>::type;
+    XT X[NSET][C];
     float FI[NSET], GI[NSET];           // row weights of the set's u row (uniform)
     __amdgpu_buffer_rsrc_t xrs[C];      // one buffer descriptor per input channel plane
 #pragma unroll
@@ -527,16 +547,20 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
 #pragma unroll
     for (int k = 0; k < NSET; ++k) FI[k] = GI[k] = 0.f;
 
-    auto issue = [&](auto SETc, int r) {       // loads for u row r into set SET
+    auto issue = [&](auto SETc, uint4 t) {     // loads for the u row of table entry t
         constexpr int SET = decltype(SETc)::value;
-        const uint4 t = lut[r - ubase];          // uniform address: LDS broadcast
         const unsigned r0 = uniform((int)t.x), r1 = uniform((int)t.y);
         FI[SET] = __builtin_bit_cast(float, uniform((int)t.z));
         GI[SET] = __builtin_bit_cast(float, uniform((int)t.w));
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            X[SET][0][c] = buf_load<Tin>(xrs[c], lbyte, r0);
-            X[SET][1][c] = buf_load<Tin>(xrs[c], lbyte, r1);
+            if constexpr (X16) {
+                X[SET][c] = u16x2{buf_load<unsigned short>(xrs[c], lbyte, r0),
+                                  buf_load<unsigned short>(xrs[c], lbyte, r1)};
+            } else {
+                X[SET][c][0] = buf_load<Tin>(xrs[c], lbyte, r0);
+                X[SET][c][1] = buf_load<Tin>(xrs[c], lbyte, r1);
+            }
         }
     };
 
@@ -563,11 +587,21 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
         float uv[C];
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            const float x0 = to_acc<float>(X[SET][0][c]);
-            const float x1 = to_acc<float>(X[SET][1][c]);
+            float x0, x1;
+            if constexpr (X16) {
+                x0 = to_acc<float>(__builtin_bit_cast(Tin, (unsigned short)X[SET][c].x));
+                x1 = to_acc<float>(__builtin_bit_cast(Tin, (unsigned short)X[SET][c].y));
+            } else {
+                x0 = to_acc<float>(X[SET][c][0]);
+                x1 = to_acc<float>(X[SET][c][1]);
+            }
             const float v = fmaf(FI[SET], x1, GI[SET] * x0);         // t = fi*p3 + (1-fi)*p1
-            const float vp = dpp_next(v), vq = dpp_next(vp);
-            const float u = fmaf(wr[0], dpp_prev(v), fmaf(wr[1], v, fmaf(wr[2], vp, wr[3] * vq)));
+            const float vp = dpp_next(v);
+            float u;
+            if constexpr (R3)
+                u = fmaf(wr[0], dpp_prev(v), fmaf(wr[1], v, wr[2] * vp));
+            else
+                u = fmaf(wr[0], dpp_prev(v), fmaf(wr[1], v, fmaf(wr[2], vp, wr[3] * dpp_next(vp))));
             uv[c] = uok ? u : colpad;                                 // pad rows / cols
         }
         float sh[NS][C];                // lane shifts -1 .. DKMAX-1 of every channel
@@ -612,7 +646,7 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
         for (int i = 0; i < O * CG * 7; ++i) wk[i] = kv[i];
     }
 #pragma unroll
-    for (int o = 0; o < O; ++o) bs[o] = bias ? bias[o + vz] : 0.f;
+    for (int o = 0; o < O; ++o) bs[o] = bias ? bias[o] : 0.f;     // scalar loads: SGPRs
 
     // HexConv2d row a2 from the u slots
     auto conv_row = [&](auto PHc, int a2, float* z) {
@@ -652,10 +686,13 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
         }
     };
 
-    // one output row a2 (phase PH = a2 % 6): u row a2+1 lives in set (PH + 1) % 3
+    // one output row a2 (phase PH = a2 % 6): u row a2+1 lives in set (PH + 1) % NSET.
+    // The table entry of the row issued at a step is read from LDS one step earlier.
+    uint4 tl[2];
     auto step = [&](auto PHc, int a2) {
         constexpr int PH = decltype(PHc)::value;
-        issue(std::integral_constant<int, (PH + 1 + PD) % NSET>{}, a2 + 1 + PD);
+        issue(std::integral_constant<int, (PH + 1 + PD) % NSET>{}, tl[PH & 1]);
+        tl[(PH + 1) & 1] = lut[a2 + 2 + PD - ubase];
         compute_u(std::integral_constant<int, (PH + 1) % 3>{},
                   std::integral_constant<int, (PH + 1) % NSET>{}, a2 + 1);
         float z[O];
@@ -672,14 +709,24 @@ __global__ __launch_bounds__(PL_THREADS) void k_pipeline_s(const Tin* __restrict
         }
     };
 
-    // prologue: u rows a2_begin-1 (slot 2) and a2_begin (slot 0), loads PD rows ahead
-    // (u row r uses set r % 3; a2_begin % 3 == 0)
-    issue(std::integral_constant<int, 2>{}, a2_begin - 1);
-    issue(std::integral_constant<int, 0>{}, a2_begin);
-    issue(std::integral_constant<int, 1>{}, a2_begin + 1);
-    compute_u(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, a2_begin - 1);
-    issue(std::integral_constant<int, 2>{}, a2_begin + 2);
-    compute_u(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, a2_begin);
+    // prologue: u rows a2_begin-1 (slot 2) and a2_begin (slot 0), rect rows of u rows up
+    // to a2_begin + PD in flight (u row r uses set (r - a2_begin) mod NSET)
+    using I0 = std::integral_constant<int, 0>;
+    using I2 = std::integral_constant<int, 2>;
+    issue(std::integral_constant<int, NSET - 1>{}, lut[0]);
+    issue(I0{}, lut[1]);
+    issue(std::integral_constant<int, 1>{}, lut[2]);
+    if constexpr (NSET == 3) {          // PD == 2: set 2 is reused by u row a2_begin + 2
+        compute_u(I2{}, I2{}, a2_begin - 1);
+        issue(I2{}, lut[3]);
+    } else {
+        issue(I2{}, lut[3]);
+        if constexpr (PD >= 3) issue(std::integral_constant<int, 3>{}, lut[4]);
+        if constexpr (PD >= 4) issue(std::integral_constant<int, 4>{}, lut[5]);
+        compute_u(I2{}, std::integral_constant<int, NSET - 1>{}, a2_begin - 1);
+    }
+    compute_u(I0{}, I0{}, a2_begin);
+    tl[0] = lut[PD + 2];                // u row a2_begin + 1 + PD
     for (int base = a2_begin; base < a2_end; base += 6) {
         step(std::integral_constant<int, 0>{}, base);
         if (base + 1 >= a2_end) break;
@@ -705,6 +752,20 @@ static void r2h_offsets(const Geom& g, int* lo, int* hi) {
     for (int64_t q = 0; q < g.w1; ++q) {
         const double j_ = axis_at(g.ys, q) + (double)(g.w - 1) * 0.5;
         const int64_t jn = (int64_t)j_;
+        mn = (int)std::min<int64_t>(mn, jn - q);
+        mx = (int)std::max<int64_t>(mx, jn - q);
+    }
+    *lo = mn; *hi = mx;
+}
+
+// The same over the columns with at least one r2h tap (jn or jn+1) inside [0, w): a
+// column with none reads zeros whatever the window (used by the static kernel).
+static void r2h_offsets_live(const Geom& g, int* lo, int* hi) {
+    int mn = INT_MAX, mx = INT_MIN;
+    for (int64_t q = 0; q < g.w1; ++q) {
+        const double j_ = axis_at(g.ys, q) + (double)(g.w - 1) * 0.5;
+        const int64_t jn = (int64_t)j_;
+        if (!((jn >= 0 && jn < g.w) || (jn + 1 >= 0 && jn + 1 < g.w))) continue;
         mn = (int)std::min<int64_t>(mn, jn - q);
         mx = (int)std::max<int64_t>(mx, jn - q);
     }
@@ -749,9 +810,12 @@ static int launch_pipeline(const void* x, const float* k, const float* bias, voi
                        k, bias, yp, F)
     // mode: 0 generic (bpermute), 1 DPP windows, 2 DPP windows + rows on hex rows,
     // 3 same-size static pipeline
-    if (mode == 3) {
-        if (F.op) hipLaunchKernelGGL((k_pipeline_s<Tin, Tout, C, O, G, 1>), grid, blk, 0, st, xp, k, bias, yp, F);
-        else hipLaunchKernelGGL((k_pipeline_s<Tin, Tout, C, O, G, 0>), grid, blk, 0, st, xp, k, bias, yp, F);
+    if (mode == 3 || mode == 4) {       // 4: static with the 3-tap r2h window
+#define HG_PLS(OPV, R3V) hipLaunchKernelGGL((k_pipeline_s<Tin, Tout, C, O, G, OPV, R3V>), grid, \
+                                            blk, 0, st, xp, k, bias, yp, F)
+        if (mode == 4) { if (F.op) HG_PLS(1, true); else HG_PLS(0, true); }
+        else { if (F.op) HG_PLS(1, false); else HG_PLS(0, false); }
+#undef HG_PLS
     } else if (mode == 2) { if (F.op) HG_PL(1, true, true); else HG_PL(0, true, true); }
     else if (mode == 1) { if (F.op) HG_PL(1, true, false); else HG_PL(0, true, false); }
     else { if (F.op) HG_PL(1, false, false); else HG_PL(0, false, false); }
@@ -816,6 +880,16 @@ extern "C" int hg_pipeline_r2h_conv_h2r(const void* x, const float* kernel, cons
         rlo = PL_RLO; rhi = PL_RHI; zlo_off = -1; zhi_off = dkmax - 1;
         olo = PL_ZBLO; ohi = PL_ZAHI;
     }
+    // mode 3: exactly same-size h2r (closed-form 2-tap rows), padding 1, DPP r2h window
+    const bool stat = dpp && identity_rows && h2 == F.ho && w2 == F.wo;
+    bool r3 = false;
+    if (stat) {
+        int llo, lhi;
+        r2h_offsets_live(F.r2h, &llo, &lhi);
+        r3 = llo >= -1 && lhi + 1 <= 1;
+        if (r3) rhi = 1;
+        olo = -1; ohi = 1;                   // 0.75 / 0.25 taps at b-1 .. b+1
+    }
     const int u_lo = std::max(0, -rlo), u_hi = std::min(63, 63 - rhi);
     const int z_lo = u_lo - std::min(zlo_off, 0), z_hi = u_hi - std::max(zhi_off, 0);
     const int o_lo = z_lo - std::min(olo, 0), o_hi = z_hi - std::max(ohi, 0);
@@ -823,11 +897,9 @@ extern "C" int hg_pipeline_r2h_conv_h2r(const void* x, const float* kernel, cons
     F.HL = o_lo;
     F.nown = o_hi - o_lo + 1;
     F.nwin = (int)((w2 + F.nown - 1) / F.nown);
-    // mode 3: exactly same-size h2r (closed-form 2-tap rows), padding 1, DPP r2h window
-    const bool stat = dpp && identity_rows && h2 == F.ho && w2 == F.wo;
     F.RB = stat ? 126 : 128;                 // static path: bands start at multiples of 6
     F.nband = (int)((h2 + F.RB - 1) / F.RB);
-    const int mode = stat ? 3 : (dpp ? (on_rows ? 2 : 1) : 0);
+    const int mode = stat ? (r3 ? 4 : 3) : (dpp ? (on_rows ? 2 : 1) : 0);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     switch (x_dtype) {
     case HG_BF16:
