@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void k_hexconv_stream(const Tin* __restrict__ 
         constexpr int SLT[3] = {PH % 3, (PH + 1) % 3, (PH + 2) % 3};   // P rows ro, ro+1, ro+2
         issue(std::integral_constant<int, (PH + 2 + PD) % NSET>{}, ro + 2 + PD);
         fill(std::integral_constant<int, (PH + 2) % 3>{}, std::integral_constant<int, (PH + 2) % NSET>{});
-        const unsigned ob = (unsigned)(ro * F.wo) * (unsigned)sizeof(Tout);
+        const unsigned ob = (unsigned)__builtin_amdgcn_readfirstlane(ro * F.wo) * (unsigned)sizeof(Tout);
         if constexpr (PK) {
 #pragma unroll
             for (int o = 0; o < 3; ++o) {

@@ -432,6 +432,12 @@ __device__ __forceinline__ T buf_load(__amdgpu_buffer_rsrc_t rs, unsigned voff, 
 #ifndef PL_S_PD
 #define PL_S_PD 2            // u rows whose rect rows are loaded ahead
 #endif
+#ifndef PL_S_OOBST
+#define PL_S_OOBST 0         // 1: non-owned lanes store out of range instead of branching
+#endif
+#ifndef PL_S_FIV
+#define PL_S_FIV 1           // 1: row weights as broadcast VGPR operands, 0: SGPRs
+#endif
 #ifndef PL_S_WPE
 #define PL_S_WPE 0           // min waves per SIMD requested from the register allocator
 #endif
@@ -543,15 +549,22 @@ void k_pipeline_s(const Tin* __restrict__ x, const float* __restrict__ kern,
         yrs[o] = __builtin_amdgcn_make_buffer_rsrc((void*)(yb + o * ostride), (short)0,
                                                    (int)(ostride * (int64_t)sizeof(Tout)),
                                                    0x00020000);
-    const unsigned obytecol = ocol * (unsigned)sizeof(Tout);
+    // PL_S_OOBST: lanes that do not own their column store to a byte offset past the
+    // plane (the buffer range check drops the write) instead of branching around it
+    const unsigned obytecol = (!PL_S_OOBST || own) ? ocol * (unsigned)sizeof(Tout) : 0x80000000u;
 #pragma unroll
     for (int k = 0; k < NSET; ++k) FI[k] = GI[k] = 0.f;
 
     auto issue = [&](auto SETc, uint4 t) {     // loads for the u row of table entry t
         constexpr int SET = decltype(SETc)::value;
         const unsigned r0 = uniform((int)t.x), r1 = uniform((int)t.y);
-        FI[SET] = __builtin_bit_cast(float, uniform((int)t.z));
-        GI[SET] = __builtin_bit_cast(float, uniform((int)t.w));
+        if (PL_S_FIV) {
+            FI[SET] = __builtin_bit_cast(float, t.z);      // broadcast VGPR operands
+            GI[SET] = __builtin_bit_cast(float, t.w);
+        } else {
+            FI[SET] = __builtin_bit_cast(float, uniform((int)t.z));
+            GI[SET] = __builtin_bit_cast(float, uniform((int)t.w));
+        }
 #pragma unroll
         for (int c = 0; c < C; ++c) {
             if constexpr (X16) {
@@ -705,7 +718,7 @@ void k_pipeline_s(const Tin* __restrict__ x, const float* __restrict__ kern,
                 out = fmaf(0.75f, z[o], 0.25f * dpp_next(z[o]));
             else                           // odd row: 0.25 z[b-1] + 0.75 z[b]
                 out = fmaf(0.25f, dpp_prev(z[o]), 0.75f * z[o]);
-            if (own) buf_store<Tout>(from_acc<Tout>(out), yrs[o], obytecol, obyte);
+            if (PL_S_OOBST || own) buf_store<Tout>(from_acc<Tout>(out), yrs[o], obytecol, obyte);
         }
     };
 
@@ -881,7 +894,9 @@ extern "C" int hg_pipeline_r2h_conv_h2r(const void* x, const float* kernel, cons
         olo = PL_ZBLO; ohi = PL_ZAHI;
     }
     // mode 3: exactly same-size h2r (closed-form 2-tap rows), padding 1, DPP r2h window
-    const bool stat = dpp && identity_rows && h2 == F.ho && w2 == F.wo;
+    // (32-bit buffer offsets: planes below 2 GiB; a dropped store's offset is 2^31)
+    const bool stat = dpp && identity_rows && h2 == F.ho && w2 == F.wo &&
+                      h * w * 8 < ((int64_t)1 << 31) && h2 * w2 * 8 < ((int64_t)1 << 31);
     bool r3 = false;
     if (stat) {
         int llo, lhi;
