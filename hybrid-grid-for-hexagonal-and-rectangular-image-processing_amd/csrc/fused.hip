@@ -1,0 +1,470 @@
+// fused.hip — streaming rect -> hex -> HexConv2d(r=2) -> hex -> rect pass, two
+// columns per lane (the headline path of hg_pipeline_r2h_conv_h2r).
+//
+// The reference chains rect_to_hex_resample (geometry_np.py:358-519, bilinear),
+// HexConv2d (HexFrames.py:96-169, radius 2, stride 1, padding 1, constant 0) and
+// hex_to_rect_resample (geometry_np.py:191-356, linear).  This kernel covers the
+// geometry every same-size round trip has, and checks it on the host:
+//   * r2h rows:    u row r blends rect rows in(r), in(r)+1 with in(r) - r in {-1, 0}
+//                  wherever a tap is inside the raster (geometry_np.py:440-486);
+//   * r2h columns: hex column q blends rect columns jn, jn+1 with jn - q in {-1, 0};
+//   * h2r:         (h2, w2) == (ho, wo), so the triangle lattice is exact:
+//                  i_ = a, j_ = 0.5a + b + 0.25 (:276-277) -> even rows
+//                  0.75 z[b] + 0.25 z[b+1], odd rows 0.25 z[b-1] + 0.75 z[b] (:347-354).
+// Everything else goes to pipeline.hip's kernels.
+//
+// Execution model.  One wavefront owns a 128-column window (lane l <-> columns
+// W0 + 2l, W0 + 2l + 1 in every stage's column space) of one image and walks a band
+// of 126 output rows.  Per output row a2 (one "step"):
+//   1. rect row a2+2 arrives in registers (loaded PD steps earlier; every rect row is
+//      loaded exactly once — a 3-row register ring, not a (in, in+1) pair per row);
+//   2. v = a*x[r-1] + b*x[r] + c*x[r+1] for u row r = a2+1 (uniform row weights from a
+//      per-wave LDS table, validity folded in);
+//   3. u = wl*v[q-1] + wc*v[q] + wr*v[q+1] (per-column weights; the neighbour columns
+//      are the lane's other column or one DPP wave shift away);
+//   4. u row r is scattered into the three conv rows it feeds (r-1 below, r centre,
+//      r+1 above; 7 taps x C x O FMAs with weights in SGPRs), so only the newest u row
+//      and three accumulator rows are live;
+//   5. conv row a2 is complete: the fixed two-tap h2r filter, cvt, one dword store per
+//      output channel (non-owned lanes store past the buffer range: dropped).
+// The step loop is unrolled by 6 = lcm(3 ring slots, 2 row parities), so ring slots
+// and tap offsets are compile-time constants and no register moves between steps.
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+#include "fused.h"
+#include "lattice.h"
+
+namespace hg {
+
+constexpr int FU_THREADS = 256;       // 4 independent waves per workgroup
+constexpr int FU_HL = 4;              // halo columns on the left of a window
+constexpr int FU_OWN = 120;           // owned columns per 128-column window
+constexpr int FU_RB = 126;            // output rows per band (multiple of 6)
+constexpr int FU_LUT = FU_RB + 2;     // u rows band_begin-1 .. band_begin+RB
+
+#ifndef FU_PD
+#define FU_PD 3                       // rect rows loaded ahead of use (1..4)
+#endif
+
+struct FusedGeom {
+    int64_t B;
+    int h, w, h1, w1, h2, w2;
+    int nwin, nband;
+    Axis rxs, rys;                    // r2h lattice axes (geometry_np.py:415-422)
+};
+
+__device__ __forceinline__ float f_prev(float v) {   // result[l] = v[l-1], 0 at lane 0
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+        __builtin_bit_cast(int, v), 0x138 /*wave_shr:1*/, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float f_next(float v) {   // result[l] = v[l+1], 0 at lane 63
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+        __builtin_bit_cast(int, v), 0x130 /*wave_shl:1*/, 0xf, 0xf, true));
+}
+
+// r=2 stencil taps (HexFrames.py:108-118 scatter into the dense 3x5 kernel):
+// row of tap t relative to the output row (0 above, 1 centre, 2 below) and its lane
+// column shift for an output row of parity `par` (type1 indexing, :417-445; derived in
+// oracle/hg_oracle.c), with padding 1: shift = dk - 1.
+__host__ __device__ constexpr int fu_tap_ii(int t) { return t < 2 ? 0 : (t < 5 ? 1 : 2); }
+__host__ __device__ constexpr int fu_tap_col(int t) {
+    return t < 2 ? 1 + 2 * t : (t < 5 ? 2 * (t - 2) : 1 + 2 * (t - 5));
+}
+__host__ __device__ constexpr int fu_tap_shift(int t, int par, int op) {
+    return ((1 + par + fu_tap_col(t) - ((((par + fu_tap_ii(t)) & 1) + op) & 1)) >> 1) - 1;
+}
+
+template <typename T> struct RawOf { using type = unsigned; };          // 2 x 16-bit
+template <> struct RawOf<float> { using type = uint2; };                // 2 x f32
+
+template <typename T>
+__device__ __forceinline__ typename RawOf<T>::type fu_load(__amdgpu_buffer_rsrc_t rs,
+                                                           unsigned voff, unsigned soff) {
+    if constexpr (sizeof(T) == 2) {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0);
+    } else {
+        typedef unsigned u2v __attribute__((ext_vector_type(2)));
+        const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+        return uint2{v.x, v.y};
+    }
+}
+template <typename T>
+__device__ __forceinline__ void fu_unpack(typename RawOf<T>::type r, float& e, float& o) {
+    if constexpr (std::is_same<T, __bf16>::value) {
+        e = __builtin_bit_cast(float, r << 16);
+        o = __builtin_bit_cast(float, r & 0xffff0000u);
+    } else if constexpr (sizeof(T) == 2) {
+        e = (float)__builtin_bit_cast(T, (unsigned short)(r & 0xffffu));
+        o = (float)__builtin_bit_cast(T, (unsigned short)(r >> 16));
+    } else {
+        e = __builtin_bit_cast(float, r.x);
+        o = __builtin_bit_cast(float, r.y);
+    }
+}
+template <typename T>
+__device__ __forceinline__ void fu_store(float e, float o, __amdgpu_buffer_rsrc_t rs,
+                                         unsigned voff, unsigned soff) {
+    if constexpr (sizeof(T) == 2) {
+        typedef T t2v __attribute__((ext_vector_type(2)));
+        const t2v p = {(T)e, (T)o};
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, p), rs, voff, soff, 0);
+    } else {
+        typedef unsigned u2v __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(
+            u2v{__builtin_bit_cast(unsigned, e), __builtin_bit_cast(unsigned, o)}, rs, voff, soff, 0);
+    }
+}
+
+template <int N> using IC = std::integral_constant<int, N>;
+__host__ __device__ constexpr int fu_mod(int a, int m) { return ((a % m) + m) % m; }
+
+template <typename Tin, typename Tout, int C, int O, int G, int OP>
+__global__ __launch_bounds__(FU_THREADS) void k_fused(const Tin* __restrict__ x,
+                                                      const float* __restrict__ kern,
+                                                      const float* __restrict__ bias,
+                                                      Tout* __restrict__ y, FusedGeom F) {
+    constexpr int CG = C / G, OG = O / G;
+    constexpr int PD = FU_PD;
+    static_assert(PD >= 1 && PD <= 4, "raw ring holds PD + 1 <= 6 rows");
+    using Raw = typename RawOf<Tin>::type;
+
+    // per-wave u-row table {a, b, c, -}: u[r] = a*x[r-1] + b*x[r] + c*x[r+1]
+    __shared__ float4 lut_all[FU_THREADS / 64][FU_LUT];
+    const int lane = threadIdx.x & 63;
+    const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float4* lut = lut_all[wslot];
+    const int64_t wave = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (FU_THREADS / 64) + wslot;
+    const int win = (int)(wave % F.nwin);
+    const int64_t rest = wave / F.nwin;
+    const int band = (int)(rest % F.nband);
+    const int64_t b = rest / F.nband;
+    if (b >= F.B) return;
+    const int W0 = win * FU_OWN - FU_HL;
+    const int ce = W0 + 2 * lane;                 // this lane's even column; odd = ce + 1
+    const int s0 = band * FU_RB;                  // first output row of the band
+    const int s1 = min(s0 + FU_RB, F.h2);
+
+    // ---- row table (fp64 lattice math, geometry_np.py:440-486) -------------
+    for (int e = lane; e < FU_LUT; e += 64) {
+        const int r = s0 - 1 + e;                 // u row
+        float4 t = {0.f, 0.f, 0.f, 0.f};
+        if (r >= 0 && r < F.h1) {
+            const double i_ = axis_at(F.rxs, r) + (double)(F.h - 1) * 0.5;   // :440
+            const int in = (int)i_;                                          // :444
+            const double f = i_ - (double)(float)in;                         // :448
+            const float w0 = (in >= 0 && in < F.h) ? (float)(1.0 - f) : 0.f;
+            const float w1 = (in + 1 >= 0 && in + 1 < F.h) ? (float)f : 0.f;
+            if (in == r - 1) { t.x = w0; t.y = w1; }
+            else if (in == r) { t.y = w0; t.z = w1; }
+        }
+        lut[e] = t;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): own-wave LDS writes
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- per-lane column weights --------------------------------------------
+    // r2h (geometry_np.py:441-449, 514-517): u[q] = sum_k wr_k[q] v[q+k], k = -1..1
+    float we[3] = {0.f, 0.f, 0.f}, wo_[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int q = ce + s;
+        float* wr = s ? wo_ : we;
+        if (q >= 0 && q < F.w1) {
+            const double j_ = axis_at(F.rys, q) + (double)(F.w - 1) * 0.5;   // :441
+            const int jn = (int)j_;
+            const double jf = j_ - (double)(float)jn;
+#pragma unroll
+            for (int k = -1; k <= 1; ++k) {
+                const bool in_w = q + k >= 0 && q + k < F.w;
+                if (k == jn - q && in_w) wr[k + 1] += (float)(1.0 - jf);
+                if (k == jn + 1 - q && in_w) wr[k + 1] += (float)jf;
+            }
+        }
+    }
+    // h2r neighbour weights with the raster edge folded in (outside -> 0, :303-323)
+    const float wn_e = (ce + 1 < F.w2) ? 0.25f : 0.f;   // even row, z[b+1], b = ce
+    const float wn_o = (ce + 2 < F.w2) ? 0.25f : 0.f;   // even row, z[b+1], b = ce+1
+    const float wp_e = (ce - 1 >= 0) ? 0.25f : 0.f;     // odd row,  z[b-1], b = ce
+    const float wp_o = (ce >= 0) ? 0.25f : 0.f;         // odd row,  z[b-1], b = ce+1
+    const bool own = lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2 && ce >= 0 && ce < F.w2;
+
+    // ---- buffers: one descriptor per image, planes by per-lane offsets ---------
+    const int64_t cstride = (int64_t)F.h * F.w, ostride = (int64_t)F.h2 * F.w2;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + b * C * cstride), (short)0, (int)(C * cstride * (int64_t)sizeof(Tin)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(y + b * O * ostride), (short)0, (int)(O * ostride * (int64_t)sizeof(Tout)), 0x00020000);
+    const int lc = min(max(ce, 0), F.w - 2);            // clamped even load column
+    unsigned xoff[C], yoff[O];
+#pragma unroll
+    for (int c = 0; c < C; ++c) xoff[c] = (unsigned)((c * cstride + lc) * (int64_t)sizeof(Tin));
+#pragma unroll
+    for (int o = 0; o < O; ++o)
+        yoff[o] = own ? (unsigned)((o * ostride + ce) * (int64_t)sizeof(Tout)) : 0x80000000u;
+    const unsigned xrow = (unsigned)F.w * (unsigned)sizeof(Tin);
+    const unsigned yrow = (unsigned)F.w2 * (unsigned)sizeof(Tout);
+    auto row_off = [&](int k) -> unsigned {             // clamped rect row (SALU)
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(k, 0), F.h - 1) * xrow));
+    };
+
+    // ---- weights: SGPRs (uniform loads); bias as VGPR addends ----------------
+    float wk[O * CG * 7];
+#pragma unroll
+    for (int i = 0; i < O * CG * 7; ++i) wk[i] = kern[i];
+    int vz = 0;
+    asm volatile("" : "+v"(vz));
+    float bv[O];
+#pragma unroll
+    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] : 0.f;
+
+    // ---- state -----------------------------------------------------------------
+    Raw raw[6][C];                      // rect rows in flight, slot (row - s0) % 6
+    float XE[3][C], XO[3][C];           // rect rows as f32, slot (row - s0) % 3
+    float ZE[3][O], ZO[3][O];           // conv rows being accumulated, slot (row - s0) % 3
+
+    auto issue = [&](auto SLc, int k) {
+        constexpr int SL = decltype(SLc)::value;
+        const unsigned so = row_off(k);
+#pragma unroll
+        for (int c = 0; c < C; ++c) raw[SL][c] = fu_load<Tin>(xrs, xoff[c], so);
+    };
+    auto convert = [&](auto RSc, auto XSc) {
+        constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
+#pragma unroll
+        for (int c = 0; c < C; ++c) fu_unpack<Tin>(raw[RS][c], XE[XS][c], XO[XS][c]);
+    };
+
+    // u row r (= s0 + PH + 1) from rect rows r-1, r, r+1 (ring slots PH, PH+1, PH+2
+    // mod 3) with table entry L, scattered into conv rows r+1 (above role; slot
+    // PH+2, started with the bias), r (centre; slot PH+1) and r-1 (below; slot PH).
+    auto urow = [&](auto PHc, float4 L, auto CENc, auto BELc) {
+        constexpr int PH = decltype(PHc)::value;
+        constexpr bool CEN = decltype(CENc)::value, BEL = decltype(BELc)::value;
+        constexpr int S0 = fu_mod(PH, 3), S1 = fu_mod(PH + 1, 3), S2 = fu_mod(PH + 2, 3);
+        constexpr int PB = fu_mod(PH, 2);       // parity of conv row r-1 (and r+1)
+        constexpr int PC = 1 - PB;              // parity of conv row r
+        float ue[C], uo[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const float ve = fmaf(L.z, XE[S2][c], fmaf(L.y, XE[S1][c], L.x * XE[S0][c]));
+            const float vo = fmaf(L.z, XO[S2][c], fmaf(L.y, XO[S1][c], L.x * XO[S0][c]));
+            const float vpo = f_prev(vo), vne = f_next(ve);
+            ue[c] = fmaf(we[2], vo, fmaf(we[1], ve, we[0] * vpo));
+            uo[c] = fmaf(wo_[2], vne, fmaf(wo_[1], vo, wo_[0] * ve));
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            // u at column offsets -1 .. 2 of each of the lane's two columns
+            const float pe = f_prev(uo[c]);     // even col - 1
+            const float ne = f_next(ue[c]);     // odd col + 1 (= even col + 2)
+            const float no = OP == 0 ? f_next(uo[c]) : 0.f;   // odd col + 2
+            auto at_e = [&](int s) { return s == -1 ? pe : (s == 0 ? ue[c] : (s == 1 ? uo[c] : ne)); };
+            auto at_o = [&](int s) { return s == -1 ? ue[c] : (s == 0 ? uo[c] : (s == 1 ? ne : no)); };
+            const int g = c / CG, ci = c % CG;
+#pragma unroll
+            for (int oo = 0; oo < OG; ++oo) {
+                const int o = g * OG + oo;
+                const float* w = &wk[(o * CG + ci) * 7];
+                // above role (taps with ii == 0) of conv row r+1, parity PB
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const int s = fu_tap_shift(t, PB, OP);
+                    if (ci == 0 && t == 0) {
+                        ZE[S2][o] = fmaf(w[t], at_e(s), bv[o]);
+                        ZO[S2][o] = fmaf(w[t], at_o(s), bv[o]);
+                    } else {
+                        ZE[S2][o] = fmaf(w[t], at_e(s), ZE[S2][o]);
+                        ZO[S2][o] = fmaf(w[t], at_o(s), ZO[S2][o]);
+                    }
+                }
+                if constexpr (CEN) {
+#pragma unroll
+                    for (int t = 2; t < 5; ++t) {
+                        const int s = fu_tap_shift(t, PC, OP);
+                        ZE[S1][o] = fmaf(w[t], at_e(s), ZE[S1][o]);
+                        ZO[S1][o] = fmaf(w[t], at_o(s), ZO[S1][o]);
+                    }
+                }
+                if constexpr (BEL) {
+#pragma unroll
+                    for (int t = 5; t < 7; ++t) {
+                        const int s = fu_tap_shift(t, PB, OP);
+                        ZE[S0][o] = fmaf(w[t], at_e(s), ZE[S0][o]);
+                        ZO[S0][o] = fmaf(w[t], at_o(s), ZO[S0][o]);
+                    }
+                }
+            }
+        }
+    };
+
+    // conv row a2 (slot PH % 3, parity PH % 2) -> output row a2 (exact same-size h2r)
+    auto out_row = [&](auto PHc, int a2) {
+        constexpr int PH = decltype(PHc)::value;
+        constexpr int S0 = PH % 3;
+        const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
+#pragma unroll
+        for (int o = 0; o < O; ++o) {
+            const float ze = ZE[S0][o], zo = ZO[S0][o];
+            float oe, oo;
+            if constexpr ((PH & 1) == 0) {      // 0.75 z[b] + 0.25 z[b+1]
+                oe = fmaf(wn_e, zo, 0.75f * ze);
+                oo = fmaf(wn_o, f_next(ze), 0.75f * zo);
+            } else {                            // 0.25 z[b-1] + 0.75 z[b]
+                oe = fmaf(wp_e, f_prev(zo), 0.75f * ze);
+                oo = fmaf(wp_o, ze, 0.75f * zo);
+            }
+            fu_store<Tout>(oe, oo, yrs, yoff[o], so);
+        }
+    };
+
+    // ---- prologue: u rows s0-1 and s0 -------------------------------------------
+    {
+        Raw t0[C], t1[C], t2[C];
+        const unsigned o0 = row_off(s0 - 2), o1 = row_off(s0 - 1), o2 = row_off(s0);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            t0[c] = fu_load<Tin>(xrs, xoff[c], o0);
+            t1[c] = fu_load<Tin>(xrs, xoff[c], o1);
+            t2[c] = fu_load<Tin>(xrs, xoff[c], o2);
+        }
+        issue(IC<1>{}, s0 + 1);
+#pragma unroll
+        for (int i = 0; i < PD; ++i) {          // ring: rect rows s0+2 .. s0+1+PD
+            if (i == 0) issue(IC<2>{}, s0 + 2);
+            if (i == 1) issue(IC<3>{}, s0 + 3);
+            if (i == 2) issue(IC<4>{}, s0 + 4);
+            if (i == 3) issue(IC<5>{}, s0 + 5);
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            fu_unpack<Tin>(t0[c], XE[1][c], XO[1][c]);   // row s0-2 -> slot 1
+            fu_unpack<Tin>(t1[c], XE[2][c], XO[2][c]);   // row s0-1 -> slot 2
+            fu_unpack<Tin>(t2[c], XE[0][c], XO[0][c]);   // row s0   -> slot 0
+        }
+    }
+    urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});   // u row s0-1: above only
+    convert(IC<1>{}, IC<1>{});                                      // row s0+1 -> slot 1
+    urow(IC<-1>{}, lut[1], std::true_type{}, std::false_type{});    // u row s0: above, centre
+
+    // ---- main loop ---------------------------------------------------------------
+    float4 lnext = lut[2];
+    auto step = [&](auto PHc, int a2) {
+        constexpr int PH = decltype(PHc)::value;
+        convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row a2+2
+        issue(IC<(PH + 2 + PD) % 6>{}, a2 + 2 + PD);
+        const float4 L = lnext;
+        lnext = lut[min(a2 - s0 + 3, FU_LUT - 1)];
+        urow(PHc, L, std::true_type{}, std::true_type{});           // u row a2+1
+        out_row(PHc, a2);
+    };
+    for (int base = s0; base < s1; base += 6) {
+        step(IC<0>{}, base);
+        if (base + 1 >= s1) break;
+        step(IC<1>{}, base + 1);
+        if (base + 2 >= s1) break;
+        step(IC<2>{}, base + 2);
+        if (base + 3 >= s1) break;
+        step(IC<3>{}, base + 3);
+        if (base + 4 >= s1) break;
+        step(IC<4>{}, base + 4);
+        if (base + 5 >= s1) break;
+        step(IC<5>{}, base + 5);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+template <typename Tin, typename Tout, int C, int O, int G>
+static int fused_launch(const void* x, const float* k, const float* bias, void* y,
+                        const FusedGeom& F, int op, hipStream_t st) {
+    const int64_t waves = F.B * (int64_t)F.nband * F.nwin;
+    const int64_t blocks = (waves + 3) / 4;
+    if (blocks > INT_MAX) return HG_ESHAPE;
+    const dim3 grid((unsigned)blocks), blk(FU_THREADS);
+    if (op)
+        hipLaunchKernelGGL((k_fused<Tin, Tout, C, O, G, 1>), grid, blk, 0, st, (const Tin*)x, k,
+                           bias, (Tout*)y, F);
+    else
+        hipLaunchKernelGGL((k_fused<Tin, Tout, C, O, G, 0>), grid, blk, 0, st, (const Tin*)x, k,
+                           bias, (Tout*)y, F);
+    return launch_status();
+}
+
+template <typename Tin, typename Tout>
+static int fused_channels(const void* x, const float* k, const float* b, void* y,
+                          const FusedGeom& F, int C, int O, int G, int op, hipStream_t st) {
+    if (C == 3 && O == 3 && G == 1) return fused_launch<Tin, Tout, 3, 3, 1>(x, k, b, y, F, op, st);
+    if (C == 3 && O == 3 && G == 3) return fused_launch<Tin, Tout, 3, 3, 3>(x, k, b, y, F, op, st);
+    if (C == 1 && O == 1 && G == 1) return fused_launch<Tin, Tout, 1, 1, 1>(x, k, b, y, F, op, st);
+    return HG_EUNSUP;
+}
+
+// Does the same-size streaming kernel cover this call?  All checks are exact on the
+// lattice the kernel would compute (O(h1 + w1) fp64 on the host).
+static bool fused_geometry_ok(const Geom& g) {
+    for (int64_t q = 0; q < g.w1; ++q) {            // r2h columns: jn - q in {-1, 0}
+        const double j_ = axis_at(g.ys, q) + (double)(g.w - 1) * 0.5;
+        const int64_t jn = (int64_t)j_;
+        const bool live = (jn >= 0 && jn < g.w) || (jn + 1 >= 0 && jn + 1 < g.w);
+        if (live && (jn - q < -1 || jn - q > 0)) return false;
+    }
+    for (int64_t r = 0; r < g.h1; ++r) {            // r2h rows: in - r in {-1, 0}
+        const double i_ = axis_at(g.xs, r) + (double)(g.h - 1) * 0.5;
+        const int64_t in = (int64_t)i_;
+        const bool live = (in >= 0 && in < g.h) || (in + 1 >= 0 && in + 1 < g.h);
+        if (live && (in - r < -1 || in - r > 0)) return false;
+    }
+    return true;
+}
+
+int fused_try(const void* x, const float* kernel, const float* bias, void* y, int x_dtype,
+              int y_dtype, int64_t batch, int C, int O, int G, int64_t h, int64_t w,
+              int64_t h1, int64_t w1, int64_t h2, int64_t w2, int padding, int op,
+              double pad_value, hipStream_t st) {
+    if (const char* e = getenv("HYGRID_FUSED2")) {   // A/B switch for measurements
+        if (e[0] == '0') return HG_EUNSUP;
+    }
+    if (padding != 1 || pad_value != 0.0) return HG_EUNSUP;
+    if (h2 != h1 || w2 != w1) return HG_EUNSUP;       // ho = h1, wo = w1 at padding 1
+    if ((w & 1) || (w1 & 1) || w < 2 || h1 < 1) return HG_EUNSUP;   // dword column pairs
+    if (x_dtype != HG_BF16 && x_dtype != HG_F16 && x_dtype != HG_F32) return HG_EUNSUP;
+    if (y_dtype != HG_BF16 && y_dtype != HG_F16 && y_dtype != HG_F32) return HG_EUNSUP;
+    if (C * h * w * 4 >= ((int64_t)1 << 31) || O * h2 * w2 * 4 >= ((int64_t)1 << 31))
+        return HG_EUNSUP;                             // 32-bit buffer offsets
+    const Geom g = make_r2h(h, w, h1, w1);
+    if (!fused_geometry_ok(g)) return HG_EUNSUP;
+    FusedGeom F;
+    F.B = batch;
+    F.h = (int)h; F.w = (int)w; F.h1 = (int)h1; F.w1 = (int)w1; F.h2 = (int)h2; F.w2 = (int)w2;
+    F.rxs = g.xs;
+    F.rys = g.ys;
+    F.nwin = (int)((w2 + FU_OWN - 1) / FU_OWN);
+    F.nband = (int)((h2 + FU_RB - 1) / FU_RB);
+    switch (x_dtype) {
+    case HG_BF16:
+        switch (y_dtype) {
+        case HG_BF16: return fused_channels<__bf16, __bf16>(x, kernel, bias, y, F, C, O, G, op, st);
+        case HG_F32: return fused_channels<__bf16, float>(x, kernel, bias, y, F, C, O, G, op, st);
+        default: return HG_EUNSUP;
+        }
+    case HG_F16:
+        switch (y_dtype) {
+        case HG_F16: return fused_channels<_Float16, _Float16>(x, kernel, bias, y, F, C, O, G, op, st);
+        case HG_F32: return fused_channels<_Float16, float>(x, kernel, bias, y, F, C, O, G, op, st);
+        default: return HG_EUNSUP;
+        }
+    default:   // HG_F32
+        switch (y_dtype) {
+        case HG_F32: return fused_channels<float, float>(x, kernel, bias, y, F, C, O, G, op, st);
+        case HG_BF16: return fused_channels<float, __bf16>(x, kernel, bias, y, F, C, O, G, op, st);
+        default: return HG_EUNSUP;
+        }
+    }
+}
+
+}  // namespace hg

@@ -24,6 +24,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "fused.h"
 #include "lattice.h"
 
 namespace hg {
@@ -877,6 +878,12 @@ extern "C" int hg_pipeline_r2h_conv_h2r(const void* x, const float* kernel, cons
     if (!x || !y) return HG_EINVAL;
     const int C = (int)channels, O = (int)out_channels, G = groups;
     if (O * (C / G) * 7 > PL_KMAX || O > 3 || C > 3) return HG_EUNSUP;
+    {   // the two-column streaming kernel (fused.hip) where its geometry holds
+        const int rc = fused_try(x, kernel, bias, y, x_dtype, y_dtype, batch, C, O, G, h, w, h1,
+                                 w1, h2, w2, padding, F.op, pad_value,
+                                 reinterpret_cast<hipStream_t>(stream));
+        if (rc != HG_EUNSUP) return rc;
+    }
     // lane halo from the lattice maps
     int jlo, jhi, clo, chi;
     bool on_rows, identity_rows;

@@ -45,6 +45,12 @@ CASES = [
     (1, 3, 70, 130, (71, 131), (70, 130), 0, 1, 1, 0.0),
     (1, 3, 9, 7, None, None, 0, 1, 1, 0.0),
     (1, 3, 270, 480, None, None, 0, 1, 1, 0.0),
+    # two-column streaming kernel (fused.hip): even widths, padding 1, pad value 0
+    (2, 3, 130, 256, None, None, 1, 1, 1, 0.0),     # even_odd_offset 1 -> odd-row shift
+    (1, 3, 300, 500, None, None, 0, 1, 3, 0.0),     # depthwise, 3 bands x 5 windows
+    (2, 1, 128, 246, None, None, 0, 1, 1, 0.0),
+    (1, 3, 6, 4, None, None, 0, 1, 1, 0.0),         # smaller than one window / band
+    (1, 3, 127, 122, None, None, 1, 1, 3, 0.0),     # band and window edges
 ]
 
 
@@ -79,6 +85,29 @@ def test_fused_4k_bf16_matches_oracle_and_unfused():
     close(y32[1].cpu().numpy(), ref, 1e-5)
     close(y[1].float().cpu().numpy(), ref, 2 ** -8)
     close(unf.cpu().numpy(), y32.cpu().numpy().astype(np.float64), 1e-5)
+
+
+@pytest.mark.parametrize("dt_in,dt_out", [
+    (torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
+    (torch.float16, torch.float16), (torch.float16, torch.float32),
+    (torch.float32, torch.float32), (torch.float32, torch.bfloat16)])
+@pytest.mark.parametrize("off", [0, 1])
+def test_fused_two_column_kernel_dtypes(dt_in, dt_out, off, monkeypatch):
+    """fused.hip (the default same-size path) against the oracle and against the
+    one-column kernel of pipeline.hip (HYGRID_FUSED2=0) on the same data."""
+    torch.manual_seed(3)
+    conv = HexConv2d(3, 3, off, 2, padding=1, bias=True).to(DEV)
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.rand((2, 3, 200, 384), generator=gen, device=DEV).to(dt_in)
+    args = (x, conv.kernel, conv.bias, None, None, 1, 1, off, 0.0, dt_out)
+    with torch.no_grad():
+        y = ops.pipeline_r2h_conv_h2r(*args)
+        monkeypatch.setenv("HYGRID_FUSED2", "0")
+        y1 = ops.pipeline_r2h_conv_h2r(*args)
+    ref = oracle_chain(x.float(), conv, (200, 384), (200, 384))
+    tol = 1e-5 if dt_out == torch.float32 else (2 ** -8 if dt_out == torch.bfloat16 else 2 ** -11)
+    close(y.double().cpu().numpy(), ref, tol)
+    close(y.double().cpu().numpy(), y1.double().cpu().numpy(), tol)
 
 
 def test_non_identity_geometry_falls_back():
