@@ -23,7 +23,7 @@
 //   3. u = wl*v[q-1] + wc*v[q] + wr*v[q+1] (per-column weights; the neighbour columns
 //      are the lane's other column or one DPP wave shift away);
 //   4. u row r is scattered into the three conv rows it feeds (r-1 below, r centre,
-//      r+1 above; 7 taps x C x O FMAs with weights in SGPRs), so only the newest u row
+//      r+1 above; 7 taps x C x O FMAs with weights in VGPRs), so only the newest u row
 //      and three accumulator rows are live;
 //   5. conv row a2 is complete: the fixed two-tap h2r filter, cvt, one dword store per
 //      output channel (non-owned lanes store past the buffer range: dropped).
@@ -46,8 +46,21 @@ constexpr int FU_OWN = 120;           // owned columns per 128-column window
 constexpr int FU_RB = 126;            // output rows per band (multiple of 6)
 constexpr int FU_LUT = FU_RB + 2;     // u rows band_begin-1 .. band_begin+RB
 
+// Tuning knobs (compile-time; tools/build_fvariant.sh builds variants of this file).
 #ifndef FU_PD
 #define FU_PD 3                       // rect rows loaded ahead of use (1..4)
+#endif
+#ifndef FU_WPE
+#define FU_WPE 1                      // minimum waves per SIMD asked of the register allocator
+#endif
+#ifndef FU_NOMEM
+#define FU_NOMEM 0                    // diagnostic: every row load / store hits row 0 (cache-resident)
+#endif
+#ifndef FU_WSGPR
+#define FU_WSGPR 0                    // 1: conv weights in SGPRs (uniform loads) instead of VGPRs
+#endif
+#ifndef FU_DRAIN
+#define FU_DRAIN 1                    // drain the prologue's loads before the row loop
 #endif
 
 struct FusedGeom {
@@ -92,11 +105,13 @@ __device__ __forceinline__ typename RawOf<T>::type fu_load(__amdgpu_buffer_rsrc_
         return uint2{v.x, v.y};
     }
 }
+// hi16: 0xffff0000 held in a VGPR (a literal operand would halve the issue rate)
 template <typename T>
-__device__ __forceinline__ void fu_unpack(typename RawOf<T>::type r, float& e, float& o) {
+__device__ __forceinline__ void fu_unpack(typename RawOf<T>::type r, float& e, float& o,
+                                          unsigned hi16) {
     if constexpr (std::is_same<T, __bf16>::value) {
         e = __builtin_bit_cast(float, r << 16);
-        o = __builtin_bit_cast(float, r & 0xffff0000u);
+        o = __builtin_bit_cast(float, r & hi16);
     } else if constexpr (sizeof(T) == 2) {
         e = (float)__builtin_bit_cast(T, (unsigned short)(r & 0xffffu));
         o = (float)__builtin_bit_cast(T, (unsigned short)(r >> 16));
@@ -123,7 +138,8 @@ template <int N> using IC = std::integral_constant<int, N>;
 __host__ __device__ constexpr int fu_mod(int a, int m) { return ((a % m) + m) % m; }
 
 template <typename Tin, typename Tout, int C, int O, int G, int OP>
-__global__ __launch_bounds__(FU_THREADS) void k_fused(const Tin* __restrict__ x,
+__global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(FU_WPE)))
+void k_fused(const Tin* __restrict__ x,
                                                       const float* __restrict__ kern,
                                                       const float* __restrict__ bias,
                                                       Tout* __restrict__ y, FusedGeom F) {
@@ -208,18 +224,26 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(const Tin* __restrict__ x,
     const unsigned xrow = (unsigned)F.w * (unsigned)sizeof(Tin);
     const unsigned yrow = (unsigned)F.w2 * (unsigned)sizeof(Tout);
     auto row_off = [&](int k) -> unsigned {             // clamped rect row (SALU)
+        if (FU_NOMEM) return 0u;
         return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(k, 0), F.h - 1) * xrow));
     };
 
-    // ---- weights: SGPRs (uniform loads); bias as VGPR addends ----------------
-    float wk[O * CG * 7];
-#pragma unroll
-    for (int i = 0; i < O * CG * 7; ++i) wk[i] = kern[i];
+    // ---- weights and bias in VGPRs -------------------------------------------------
+    // A VALU instruction with an SGPR (or literal) operand issues at half rate on gfx950
+    // (4.2 vs 2.3 cycles per wave-instruction, tools/microbench/issue.hip), so every
+    // FMA operand is a VGPR: an opaque per-lane zero offset makes these vector loads.
     int vz = 0;
     asm volatile("" : "+v"(vz));
+    float wk[O * CG * 7];
+#pragma unroll
+    for (int i = 0; i < O * CG * 7; ++i) wk[i] = kern[i + (FU_WSGPR ? 0 : vz)];
     float bv[O];
 #pragma unroll
     for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] : 0.f;
+    float c75 = 0.75f;                  // h2r weight as a VGPR operand, not a literal
+    asm volatile("" : "+v"(c75));
+    unsigned hi16 = 0xffff0000u;
+    asm volatile("" : "+v"(hi16));
 
     // ---- state -----------------------------------------------------------------
     Raw raw[6][C];                      // rect rows in flight, slot (row - s0) % 6
@@ -235,7 +259,7 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(const Tin* __restrict__ x,
     auto convert = [&](auto RSc, auto XSc) {
         constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
 #pragma unroll
-        for (int c = 0; c < C; ++c) fu_unpack<Tin>(raw[RS][c], XE[XS][c], XO[XS][c]);
+        for (int c = 0; c < C; ++c) fu_unpack<Tin>(raw[RS][c], XE[XS][c], XO[XS][c], hi16);
     };
 
     // u row r (= s0 + PH + 1) from rect rows r-1, r, r+1 (ring slots PH, PH+1, PH+2
@@ -305,19 +329,19 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(const Tin* __restrict__ x,
     auto out_row = [&](auto PHc, int a2) {
         constexpr int PH = decltype(PHc)::value;
         constexpr int S0 = PH % 3;
-        const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
+        const unsigned so = FU_NOMEM ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
 #pragma unroll
         for (int o = 0; o < O; ++o) {
             const float ze = ZE[S0][o], zo = ZO[S0][o];
             float oe, oo;
             if constexpr ((PH & 1) == 0) {      // 0.75 z[b] + 0.25 z[b+1]
-                oe = fmaf(wn_e, zo, 0.75f * ze);
-                oo = fmaf(wn_o, f_next(ze), 0.75f * zo);
+                oe = fmaf(wn_e, zo, c75 * ze);
+                oo = fmaf(wn_o, f_next(ze), c75 * zo);
             } else {                            // 0.25 z[b-1] + 0.75 z[b]
-                oe = fmaf(wp_e, f_prev(zo), 0.75f * ze);
-                oo = fmaf(wp_o, ze, 0.75f * zo);
+                oe = fmaf(wp_e, f_prev(zo), c75 * ze);
+                oo = fmaf(wp_o, ze, c75 * zo);
             }
-            fu_store<Tout>(oe, oo, yrs, yoff[o], so);
+                fu_store<Tout>(oe, oo, yrs, yoff[o], so);
         }
     };
 
@@ -341,14 +365,18 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(const Tin* __restrict__ x,
         }
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            fu_unpack<Tin>(t0[c], XE[1][c], XO[1][c]);   // row s0-2 -> slot 1
-            fu_unpack<Tin>(t1[c], XE[2][c], XO[2][c]);   // row s0-1 -> slot 2
-            fu_unpack<Tin>(t2[c], XE[0][c], XO[0][c]);   // row s0   -> slot 0
+            fu_unpack<Tin>(t0[c], XE[1][c], XO[1][c], hi16);   // row s0-2 -> slot 1
+            fu_unpack<Tin>(t1[c], XE[2][c], XO[2][c], hi16);   // row s0-1 -> slot 2
+            fu_unpack<Tin>(t2[c], XE[0][c], XO[0][c], hi16);   // row s0   -> slot 0
         }
     }
     urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});   // u row s0-1: above only
     convert(IC<1>{}, IC<1>{});                                      // row s0+1 -> slot 1
     urow(IC<-1>{}, lut[1], std::true_type{}, std::false_type{});    // u row s0: above, centre
+    // Drain the prologue's loads: the compiler's wait counts at the loop header merge the
+    // entry path with the back edge, and a ring load issued late on the entry path would
+    // otherwise put a near-zero vmcnt wait into every iteration.
+    if (FU_DRAIN) __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
 
     // ---- main loop ---------------------------------------------------------------
     float4 lnext = lut[2];
@@ -361,18 +389,31 @@ __global__ __launch_bounds__(FU_THREADS) void k_fused(const Tin* __restrict__ x,
         urow(PHc, L, std::true_type{}, std::true_type{});           // u row a2+1
         out_row(PHc, a2);
     };
-    for (int base = s0; base < s1; base += 6) {
+    // Full blocks of six unconditional steps: an exit or a conditional store between
+    // steps would let the compiler sink each rect-row load (and the last FMAs of a conv
+    // row) into the rarer block that consumes them, which removes the prefetch distance
+    // and serialises the accumulation.  The band's last h2 % 6 rows run as a tail.
+    int base = s0;
+    for (; base + 6 <= s1; base += 6) {
         step(IC<0>{}, base);
-        if (base + 1 >= s1) break;
         step(IC<1>{}, base + 1);
-        if (base + 2 >= s1) break;
         step(IC<2>{}, base + 2);
-        if (base + 3 >= s1) break;
         step(IC<3>{}, base + 3);
-        if (base + 4 >= s1) break;
         step(IC<4>{}, base + 4);
-        if (base + 5 >= s1) break;
         step(IC<5>{}, base + 5);
+    }
+    if (base < s1) {
+        step(IC<0>{}, base);
+        if (base + 1 < s1) {
+            step(IC<1>{}, base + 1);
+            if (base + 2 < s1) {
+                step(IC<2>{}, base + 2);
+                if (base + 3 < s1) {
+                    step(IC<3>{}, base + 3);
+                    if (base + 4 < s1) step(IC<4>{}, base + 4);
+                }
+            }
+        }
     }
 }
 

@@ -1,0 +1,69 @@
+"""Interleaved A/B timing of fused-kernel variants in ONE process (same GPU, same clocks):
+each round launches every variant library once on the same device buffers; reports the
+median / min per-launch time over the rounds (HIP events on the launch stream).
+
+usage: python tools/ab_fused.py [rounds] name1 name2 ...   (name 'base' = the in-tree lib;
+       others = HyGrid/_lib/variants/libhygrid_<name>.so); env AB_BATCH (default 128).
+"""
+import ctypes
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "hybrid-grid-for-hexagonal-and-rectangular-image-processing_amd",
+                      "HyGrid", "_lib")
+_i64, _int, _vp, _dbl = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_double
+
+
+def load(name):
+    path = os.path.join(LIBDIR, "libhygrid_hip.so") if name == "base" else \
+        os.path.join(LIBDIR, "variants", f"libhygrid_{name}.so")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    f = lib.hg_pipeline_r2h_conv_h2r
+    f.argtypes = [_vp, _vp, _vp, _vp, _int, _int] + [_i64] * 9 + [_int, _int, _int, _dbl, _vp]
+    f.restype = _int
+    return f
+
+
+def main():
+    rounds = int(sys.argv[1])
+    names = sys.argv[2:]
+    B, C, H, W = int(os.environ.get("AB_BATCH", "128")), 3, 2160, 3840
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(2)
+    x = torch.rand((B, C, H, W), generator=g, device=dev, dtype=torch.bfloat16)
+    y = torch.empty_like(x)
+    torch.manual_seed(3)
+    k = (torch.rand((3, 21), device=dev) - 0.5) * 0.5
+    b = torch.rand((3,), device=dev) - 0.5
+    st = torch.cuda.current_stream()
+    fns = {n: load(n) for n in names}
+    args = lambda: (x.data_ptr(), k.data_ptr(), b.data_ptr(), y.data_ptr(), 7, 7, B, C, C, H, W,
+                    H, W, H, W, 1, 1, 0, 0.0, st.cuda_stream)
+    times = {n: [] for n in names}
+    sums = {}
+    for r in range(rounds + 1):
+        for n, f in fns.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = f(*args())
+            e1.record()
+            if rc != 0:
+                raise SystemExit(f"{n}: status {rc}")
+            e1.synchronize()
+            if r > 0:
+                times[n].append(e0.elapsed_time(e1))
+            if r == rounds:
+                sums[n] = float(y.float().sum().item())
+    alg = 2.0 * B * C * H * W * 2
+    for n in names:
+        t = times[n]
+        print(f"{n:14s} median {statistics.median(t):.4f} ms  min {min(t):.4f} ms  "
+              f"{alg / statistics.median(t) / 1e6:.0f} GB/s  checksum {sums[n]:.6e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

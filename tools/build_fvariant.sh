@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build a tuning variant of libhygrid_hip.so with fused.hip recompiled under extra -D
+# flags, linked with the objects of the last `make`.  Run it with HYGRID_LIB=<path>.
+#   tools/build_fvariant.sh NAME -DFU_PD=2 [-D...]
+set -euo pipefail
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+PKG=$ROOT/hybrid-grid-for-hexagonal-and-rectangular-image-processing_amd
+NAME=$1; shift
+OBJ=$PKG/build/obj
+OUT=$PKG/HyGrid/_lib/variants
+mkdir -p "$OUT" "$OBJ/variants"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize "$@" \
+    -c "$PKG/csrc/fused.hip" -o "$OBJ/variants/fused_$NAME.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libhygrid_$NAME.so" \
+    "$OBJ/abi.o" "$OBJ/resample.o" "$OBJ/hexconv.o" "$OBJ/conv_stream.o" "$OBJ/pipeline.o" "$OBJ/variants/fused_$NAME.o"
+echo "$OUT/libhygrid_$NAME.so"
