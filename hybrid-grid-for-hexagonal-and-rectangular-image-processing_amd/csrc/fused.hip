@@ -59,6 +59,12 @@ constexpr int FU_LUT = FU_RB + 2;     // u rows band_begin-1 .. band_begin+RB
 #ifndef FU_WSGPR
 #define FU_WSGPR 0                    // 1: conv weights in SGPRs (uniform loads) instead of VGPRs
 #endif
+#ifndef FU_STAGE
+#define FU_STAGE 0                    // 16-bit outputs: stage rows in LDS, store whole 128-B lines
+#endif
+#ifndef FU_SCHED
+#define FU_SCHED 0                    // 1: scheduling barrier between steps (bounds register use)
+#endif
 #ifndef FU_DRAIN
 #define FU_DRAIN 1                    // drain the prologue's loads before the row loop
 #endif
@@ -148,17 +154,27 @@ void k_fused(const Tin* __restrict__ x,
     static_assert(PD >= 1 && PD <= 4, "raw ring holds PD + 1 <= 6 rows");
     using Raw = typename RawOf<Tin>::type;
 
+    // The 4 waves of a workgroup take 4 adjacent windows of one (image, band): a group
+    // of FU_GRP owned columns.  With STAGE, output rows go through LDS and the group
+    // stores them as aligned 128-B lines (a window's 240 owned bytes are not line
+    // aligned; partial-line stores cost ~20 % of HBM throughput, tools/microbench/walk2).
+    constexpr bool STAGE = FU_STAGE && sizeof(Tout) == 2;
+    constexpr int GW = FU_THREADS / 64;             // windows per group
+    constexpr int GDW = GW * FU_OWN / 2;            // dwords of one output row of a group
     // per-wave u-row table {a, b, c, -}: u[r] = a*x[r-1] + b*x[r] + c*x[r+1]
-    __shared__ float4 lut_all[FU_THREADS / 64][FU_LUT];
+    __shared__ float4 lut_all[GW][FU_LUT];
+    __shared__ unsigned stg[STAGE ? 2 : 1][STAGE ? 6 : 1][STAGE ? O : 1][STAGE ? GDW + 4 : 1];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4* lut = lut_all[wslot];
-    const int64_t wave = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (FU_THREADS / 64) + wslot;
-    const int win = (int)(wave % F.nwin);
-    const int64_t rest = wave / F.nwin;
+    const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
+    const int ngrp = (F.nwin + GW - 1) / GW;
+    const int grp = (int)(blk % ngrp);
+    const int64_t rest = blk / ngrp;
     const int band = (int)(rest % F.nband);
     const int64_t b = rest / F.nband;
-    if (b >= F.B) return;
+    if (b >= F.B) return;                         // uniform per workgroup
+    const int win = grp * GW + wslot;             // may be >= nwin: runs, owns nothing
     const int W0 = win * FU_OWN - FU_HL;
     const int ce = W0 + 2 * lane;                 // this lane's even column; odd = ce + 1
     const int s0 = band * FU_RB;                  // first output row of the band
@@ -202,11 +218,15 @@ void k_fused(const Tin* __restrict__ x,
         }
     }
     // h2r neighbour weights with the raster edge folded in (outside -> 0, :303-323)
-    const float wn_e = (ce + 1 < F.w2) ? 0.25f : 0.f;   // even row, z[b+1], b = ce
+    // (w2 is even, so for an owned lane z[ce+1] and z[ce] are always inside: those two
+    // weights are the constant 0.25; only the outer neighbours can fall off the raster)
     const float wn_o = (ce + 2 < F.w2) ? 0.25f : 0.f;   // even row, z[b+1], b = ce+1
     const float wp_e = (ce - 1 >= 0) ? 0.25f : 0.f;     // odd row,  z[b-1], b = ce
-    const float wp_o = (ce >= 0) ? 0.25f : 0.f;         // odd row,  z[b-1], b = ce+1
-    const bool own = lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2 && ce >= 0 && ce < F.w2;
+    const bool own = lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2 && ce >= 0 && ce < F.w2 &&
+                     win < F.nwin;
+    // staging slot of this lane's two output columns (non-owned lanes write a pad dword)
+    const int sidx = (lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2)
+                         ? wslot * (FU_OWN / 2) + lane - FU_HL / 2 : GDW + (lane & 3);
 
     // ---- buffers: one descriptor per image, planes by per-lane offsets ---------
     const int64_t cstride = (int64_t)F.h * F.w, ostride = (int64_t)F.h2 * F.w2;
@@ -215,12 +235,11 @@ void k_fused(const Tin* __restrict__ x,
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(y + b * O * ostride), (short)0, (int)(O * ostride * (int64_t)sizeof(Tout)), 0x00020000);
     const int lc = min(max(ce, 0), F.w - 2);            // clamped even load column
-    unsigned xoff[C], yoff[O];
-#pragma unroll
-    for (int c = 0; c < C; ++c) xoff[c] = (unsigned)((c * cstride + lc) * (int64_t)sizeof(Tin));
-#pragma unroll
-    for (int o = 0; o < O; ++o)
-        yoff[o] = own ? (unsigned)((o * ostride + ce) * (int64_t)sizeof(Tout)) : 0x80000000u;
+    // one VGPR offset per lane; the plane of a channel is an SGPR offset
+    const unsigned xoff = (unsigned)lc * (unsigned)sizeof(Tin);
+    const unsigned yoff = own ? (unsigned)ce * (unsigned)sizeof(Tout) : 0x80000000u;
+    const unsigned xplane = (unsigned)(cstride * (int64_t)sizeof(Tin));
+    const unsigned yplane = (unsigned)(ostride * (int64_t)sizeof(Tout));
     const unsigned xrow = (unsigned)F.w * (unsigned)sizeof(Tin);
     const unsigned yrow = (unsigned)F.w2 * (unsigned)sizeof(Tout);
     auto row_off = [&](int k) -> unsigned {             // clamped rect row (SALU)
@@ -240,8 +259,8 @@ void k_fused(const Tin* __restrict__ x,
     float bv[O];
 #pragma unroll
     for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] : 0.f;
-    float c75 = 0.75f;                  // h2r weight as a VGPR operand, not a literal
-    asm volatile("" : "+v"(c75));
+    float c75 = 0.75f, c25 = 0.25f;     // h2r weights as VGPR operands, not literals
+    asm volatile("" : "+v"(c75), "+v"(c25));
     unsigned hi16 = 0xffff0000u;
     asm volatile("" : "+v"(hi16));
 
@@ -254,7 +273,7 @@ void k_fused(const Tin* __restrict__ x,
         constexpr int SL = decltype(SLc)::value;
         const unsigned so = row_off(k);
 #pragma unroll
-        for (int c = 0; c < C; ++c) raw[SL][c] = fu_load<Tin>(xrs, xoff[c], so);
+        for (int c = 0; c < C; ++c) raw[SL][c] = fu_load<Tin>(xrs, xoff, so + c * xplane);
     };
     auto convert = [&](auto RSc, auto XSc) {
         constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
@@ -326,8 +345,9 @@ void k_fused(const Tin* __restrict__ x,
     };
 
     // conv row a2 (slot PH % 3, parity PH % 2) -> output row a2 (exact same-size h2r)
-    auto out_row = [&](auto PHc, int a2) {
+    auto out_row = [&](auto PHc, auto SBc, int a2) {
         constexpr int PH = decltype(PHc)::value;
+        constexpr int SB = STAGE ? decltype(SBc)::value : 0;
         constexpr int S0 = PH % 3;
         const unsigned so = FU_NOMEM ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
 #pragma unroll
@@ -335,13 +355,50 @@ void k_fused(const Tin* __restrict__ x,
             const float ze = ZE[S0][o], zo = ZO[S0][o];
             float oe, oo;
             if constexpr ((PH & 1) == 0) {      // 0.75 z[b] + 0.25 z[b+1]
-                oe = fmaf(wn_e, zo, c75 * ze);
+                oe = fmaf(c25, zo, c75 * ze);
                 oo = fmaf(wn_o, f_next(ze), c75 * zo);
             } else {                            // 0.25 z[b-1] + 0.75 z[b]
                 oe = fmaf(wp_e, f_prev(zo), c75 * ze);
-                oo = fmaf(wp_o, ze, c75 * zo);
+                oo = fmaf(c25, ze, c75 * zo);
             }
-                fu_store<Tout>(oe, oo, yrs, yoff[o], so);
+                if constexpr (STAGE) {
+                typedef Tout t2v __attribute__((ext_vector_type(2)));
+                const t2v pk = {(Tout)oe, (Tout)oo};
+                stg[SB][PH][o][sidx] = __builtin_bit_cast(unsigned, pk);
+            } else {
+                fu_store<Tout>(oe, oo, yrs, yoff, so + o * yplane);
+            }
+        }
+    };
+
+    // Store rows base .. base+nr-1 of the group from staging buffer SB: per (row, o) the
+    // group's segment of GDW dwords, as 4 line-aligned 256-B pieces (one dword per lane;
+    // lanes outside the segment store past the buffer range).  Rows are spread over
+    // the group's waves.
+    const int gcol0 = grp * GW * FU_OWN;                          // first column of the group
+    const int gdw = max(0, min(GDW, (F.w2 - gcol0) / 2));         // valid dwords per row
+    auto flush = [&](auto SBc, int base, int nr) {
+        constexpr int SB = decltype(SBc)::value;
+        __builtin_amdgcn_s_waitcnt(0xc07f);                       // lgkmcnt(0): our writes
+        __builtin_amdgcn_s_barrier();
+        // fixed trip count (the wait counts of the following steps stay exact): pairs
+        // past nr * O store nothing
+#pragma unroll
+        for (int i = 0; i < (6 * O + GW - 1) / GW; ++i) {
+            const int p = wslot + GW * i;
+            const bool pv = p < nr * O;
+            const int row = pv ? p / O : 0, o = pv ? p - row * O : 0;
+            const unsigned S = (unsigned)((((int64_t)o * F.h2 + base + row) * F.w2 + gcol0) *
+                                          (int64_t)sizeof(Tout));
+            const unsigned A = S & ~127u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const unsigned gb = A + 256u * k + 4u * lane;
+                const int d = (int)(gb - S) / 4;
+                const bool ok = pv && gb >= S && d < gdw;
+                const unsigned v = stg[SB][row][o][ok ? d : 0];
+                __builtin_amdgcn_raw_buffer_store_b32(v, yrs, ok ? gb : 0x80000000u, 0, 0);
+            }
         }
     };
 
@@ -351,9 +408,9 @@ void k_fused(const Tin* __restrict__ x,
         const unsigned o0 = row_off(s0 - 2), o1 = row_off(s0 - 1), o2 = row_off(s0);
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            t0[c] = fu_load<Tin>(xrs, xoff[c], o0);
-            t1[c] = fu_load<Tin>(xrs, xoff[c], o1);
-            t2[c] = fu_load<Tin>(xrs, xoff[c], o2);
+            t0[c] = fu_load<Tin>(xrs, xoff, o0 + c * xplane);
+            t1[c] = fu_load<Tin>(xrs, xoff, o1 + c * xplane);
+            t2[c] = fu_load<Tin>(xrs, xoff, o2 + c * xplane);
         }
         issue(IC<1>{}, s0 + 1);
 #pragma unroll
@@ -380,40 +437,57 @@ void k_fused(const Tin* __restrict__ x,
 
     // ---- main loop ---------------------------------------------------------------
     float4 lnext = lut[2];
-    auto step = [&](auto PHc, int a2) {
+    auto step = [&](auto PHc, auto SBc, int a2) {
         constexpr int PH = decltype(PHc)::value;
+        // keep each step's instructions inside the step: across a 12-step body the
+        // scheduler otherwise hoists loads many steps ahead (266 VGPRs, 1 wave / SIMD)
+        if (FU_SCHED) __builtin_amdgcn_sched_barrier(0);
         convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row a2+2
         issue(IC<(PH + 2 + PD) % 6>{}, a2 + 2 + PD);
         const float4 L = lnext;
         lnext = lut[min(a2 - s0 + 3, FU_LUT - 1)];
         urow(PHc, L, std::true_type{}, std::true_type{});           // u row a2+1
-        out_row(PHc, a2);
+        out_row(PHc, SBc, a2);
     };
     // Full blocks of six unconditional steps: an exit or a conditional store between
     // steps would let the compiler sink each rect-row load (and the last FMAs of a conv
     // row) into the rarer block that consumes them, which removes the prefetch distance
     // and serialises the accumulation.  The band's last h2 % 6 rows run as a tail.
-    int base = s0;
-    for (; base + 6 <= s1; base += 6) {
-        step(IC<0>{}, base);
-        step(IC<1>{}, base + 1);
-        step(IC<2>{}, base + 2);
-        step(IC<3>{}, base + 3);
-        step(IC<4>{}, base + 4);
-        step(IC<5>{}, base + 5);
-    }
-    if (base < s1) {
-        step(IC<0>{}, base);
+    // Two iterations per trip so the staging buffer index is a constant.
+    auto block6 = [&](auto SBc, int base) {
+        step(IC<0>{}, SBc, base);
+        step(IC<1>{}, SBc, base + 1);
+        step(IC<2>{}, SBc, base + 2);
+        step(IC<3>{}, SBc, base + 3);
+        step(IC<4>{}, SBc, base + 4);
+        step(IC<5>{}, SBc, base + 5);
+        if constexpr (STAGE) flush(SBc, base, 6);
+    };
+    auto tail = [&](auto SBc, int base) {
+        if (base >= s1) return;
+        step(IC<0>{}, SBc, base);
         if (base + 1 < s1) {
-            step(IC<1>{}, base + 1);
+            step(IC<1>{}, SBc, base + 1);
             if (base + 2 < s1) {
-                step(IC<2>{}, base + 2);
+                step(IC<2>{}, SBc, base + 2);
                 if (base + 3 < s1) {
-                    step(IC<3>{}, base + 3);
-                    if (base + 4 < s1) step(IC<4>{}, base + 4);
+                    step(IC<3>{}, SBc, base + 3);
+                    if (base + 4 < s1) step(IC<4>{}, SBc, base + 4);
                 }
             }
         }
+        if constexpr (STAGE) flush(SBc, base, s1 - base);
+    };
+    int base = s0;
+    for (; base + 12 <= s1; base += 12) {
+        block6(IC<0>{}, base);
+        block6(IC<1>{}, base + 6);
+    }
+    if (base + 6 <= s1) {
+        block6(IC<0>{}, base);
+        tail(IC<1>{}, base + 6);
+    } else {
+        tail(IC<0>{}, base);
     }
 }
 
@@ -423,8 +497,7 @@ void k_fused(const Tin* __restrict__ x,
 template <typename Tin, typename Tout, int C, int O, int G>
 static int fused_launch(const void* x, const float* k, const float* bias, void* y,
                         const FusedGeom& F, int op, hipStream_t st) {
-    const int64_t waves = F.B * (int64_t)F.nband * F.nwin;
-    const int64_t blocks = (waves + 3) / 4;
+    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + 3) / 4);
     if (blocks > INT_MAX) return HG_ESHAPE;
     const dim3 grid((unsigned)blocks), blk(FU_THREADS);
     if (op)

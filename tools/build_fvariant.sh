@@ -10,7 +10,7 @@ OBJ=$PKG/build/obj
 OUT=$PKG/HyGrid/_lib/variants
 mkdir -p "$OUT" "$OBJ/variants"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize "$@" \
-    -c "$PKG/csrc/fused.hip" -o "$OBJ/variants/fused_$NAME.o"
+    -I"$PKG/csrc" -c "${FUSED_SRC:-$PKG/csrc/fused.hip}" -o "$OBJ/variants/fused_$NAME.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libhygrid_$NAME.so" \
     "$OBJ/abi.o" "$OBJ/resample.o" "$OBJ/hexconv.o" "$OBJ/conv_stream.o" "$OBJ/pipeline.o" "$OBJ/variants/fused_$NAME.o"
 echo "$OUT/libhygrid_$NAME.so"

@@ -22,6 +22,19 @@ __global__ __launch_bounds__(256) void k(float* out, int iters, float sv, unsign
             if (MODE == 3) asm volatile("v_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
             if (MODE == 4) asm volatile("v_mul_f32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(m));
             if (MODE == 5) asm volatile("v_mov_b32 %0, %1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
+            if (MODE == 7) asm volatile("v_dot2c_f32_f16 %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(m));
+            if (MODE == 8) asm volatile("v_dot2_f32_bf16 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(m));
+            if (MODE == 9) asm volatile("v_dot2c_f32_bf16 %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(m));
+            if (MODE == 10) asm volatile("v_pk_fma_f16 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(m));
+            if (MODE == 11) asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 5) & 7]));
+            if (MODE == 12) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 13) asm volatile("v_mul_f32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 14) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 15) asm volatile("v_lshlrev_b32 %0, 16, %1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
+            if (MODE == 16) asm volatile("v_and_b32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 17) asm volatile("v_add_f32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 18) asm volatile("v_fmac_f32 %0, 0.5, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 7]));
+            if (MODE == 19) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(*(double*)&a[(2 * i) & 7]) : "v"(*(double*)&a[(2 * i + 2) & 7]), "v"(*(double*)&a[(2 * i + 4) & 7]));
             if (MODE == 6) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[i]) : "s"(sv), "v"(a[(i + 1) & 7]));
         }
     }
@@ -54,11 +67,13 @@ int main() {
     float* o; unsigned long long* clk;
     CK(hipMalloc(&o, (size_t)1024 * 8 * 256 * 4)); CK(hipMalloc(&clk, (size_t)1024 * 8 * 16));
     run<0>("v_fmac_f32 v,v", o, clk);
-    run<1>("v_fmac_f32 s,v", o, clk);
-    run<6>("v_fma_f32 s,v,v (VOP3)", o, clk);
+    run<13>("v_mul_f32 v,v", o, clk);
+    run<14>("v_fma_f32 v,v,v (VOP3)", o, clk);
+    run<17>("v_add_f32 v,v", o, clk);
+    run<15>("v_lshlrev_b32 16,v", o, clk);
+    run<16>("v_and_b32 v,v", o, clk);
+    run<18>("v_fmac_f32 inline-const", o, clk);
+    run<19>("v_pk_fma_f32 v", o, clk);
     run<5>("v_mov_b32", o, clk);
-    run<2>("v_mov_b32_dpp wave_shr:1", o, clk);
-    run<3>("v_mov_b32_dpp row_shr:1", o, clk);
-    run<4>("v_mul_f32_dpp wave_shr:1", o, clk);
     return 0;
 }
