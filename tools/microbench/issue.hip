@@ -35,6 +35,17 @@ __global__ __launch_bounds__(256) void k(float* out, int iters, float sv, unsign
             if (MODE == 17) asm volatile("v_add_f32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(a[(i + 2) & 7]));
             if (MODE == 18) asm volatile("v_fmac_f32 %0, 0.5, %1" : "+v"(a[i]) : "v"(a[(i + 1) & 7]));
             if (MODE == 19) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(*(double*)&a[(2 * i) & 7]) : "v"(*(double*)&a[(2 * i + 2) & 7]), "v"(*(double*)&a[(2 * i + 4) & 7]));
+            if (MODE == 20) asm volatile("v_perm_b32 %0, %1, %2, %3" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 2) & 7]), "v"(m));
+            if (MODE == 21) asm volatile("v_alignbyte_b32 %0, %1, %2, 2" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 22) asm volatile("v_lshlrev_b32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 23) asm volatile("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 24) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
+            if (MODE == 25) asm volatile("v_cndmask_b32 %0, %1, %2, vcc" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 26) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(a[i]), "+v"(a[(i + 4) & 7]));
+            if (MODE == 27) asm volatile("v_cvt_f32_f16 %0, %1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
+            if (MODE == 28) asm volatile("v_max_f32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 2) & 7]));
+            if (MODE == 29) asm volatile("v_cvt_f32_bf16 %0, %1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
+            if (MODE == 30) asm volatile("v_cvt_f32_bf16_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
             if (MODE == 6) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[i]) : "s"(sv), "v"(a[(i + 1) & 7]));
         }
     }
@@ -67,13 +78,16 @@ int main() {
     float* o; unsigned long long* clk;
     CK(hipMalloc(&o, (size_t)1024 * 8 * 256 * 4)); CK(hipMalloc(&clk, (size_t)1024 * 8 * 16));
     run<0>("v_fmac_f32 v,v", o, clk);
-    run<13>("v_mul_f32 v,v", o, clk);
-    run<14>("v_fma_f32 v,v,v (VOP3)", o, clk);
-    run<17>("v_add_f32 v,v", o, clk);
-    run<15>("v_lshlrev_b32 16,v", o, clk);
-    run<16>("v_and_b32 v,v", o, clk);
-    run<18>("v_fmac_f32 inline-const", o, clk);
-    run<19>("v_pk_fma_f32 v", o, clk);
-    run<5>("v_mov_b32", o, clk);
+    run<20>("v_perm_b32", o, clk);
+    run<21>("v_alignbyte_b32 ,2", o, clk);
+    run<22>("v_lshlrev_b32 v,v", o, clk);
+    run<23>("v_lshlrev_b32_sdwa", o, clk);
+    run<24>("v_mov_b32_sdwa WORD_1<-WORD_0", o, clk);
+    run<25>("v_cndmask_b32 vcc", o, clk);
+    run<26>("v_permlane32_swap", o, clk);
+    run<27>("v_cvt_f32_f16", o, clk);
+    run<28>("v_max_f32", o, clk);
+    run<29>("v_cvt_f32_bf16", o, clk);
+    run<30>("v_cvt_f32_bf16_sdwa WORD_1", o, clk);
     return 0;
 }
