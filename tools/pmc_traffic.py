@@ -22,7 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGES = {   # json key -> (prof_pipeline stage, kernel-name substring)
-    "pipeline_r2h_conv_h2r": ("fused", "k_pipeline"),
+    "pipeline_r2h_conv_h2r": ("fused", "k_fused"),
     "rect_to_hex": ("r2h", "k_resample"),
     "hexconv2d": ("conv", "k_hexconv"),
     "hex_to_rect": ("h2r", "k_resample"),
