@@ -43,6 +43,8 @@ SIGNATURES = {
                                 ctypes.POINTER(_i64), ctypes.POINTER(_i64)], _int),
     "hg_hexconv2d": ([_vp, _vp, _vp, _vp, _int, _int, _int, _i64, _i64, _i64, _i64, _i64,
                       _int, _int, _int, _int, _int, _int, _int, _dbl, _vp], _int),
+    "hg_hexconv2d_backward": ([_vp] * 6 + [_int, _int] + [_i64] * 5 + [_int] * 7 + [_dbl, _vp],
+                              _int),
     "hg_pipeline_r2h_conv_h2r": ([_vp, _vp, _vp, _vp, _int, _int] + [_i64] * 9 +
                                  [_int, _int, _int, _dbl, _vp], _int),
 }

@@ -126,9 +126,42 @@ def hexconv2d(x, kernel, bias, even_odd_offset, radius, stride=1, padding=0, dil
     return y
 
 
-def hexconv2d_backward(gy, x, kernel, bias, cfg, need_x, need_k, need_b):
-    """Gradients of hexconv2d."""
-    raise NotImplementedError("HexConv2d backward kernels are not built yet")
+def hexconv2d_backward(gy, x, kernel, bias, cfg, need_x=True, need_k=True, need_b=True):
+    """Gradients of hexconv2d (hg_hexconv2d_backward): (d x, d kernel, d bias).
+
+    gy: (B, O, ho, wo); x: the forward input (B, C, H, W); kernel: the parameter
+    (O, C/groups, 1, K) (its dtype, float32 or float64, is the accumulation dtype, as
+    the forward's `input.to(self.kernel.dtype)`, HexFrames.py:107).  Returns None for
+    the gradients not requested; d x has x's dtype, d kernel / d bias the parameters'.
+    """
+    _abi.require_device(gy)
+    while x.dim() < 4:
+        x = x.unsqueeze(0)
+    x = x.contiguous()
+    B, C, h, w = (int(s) for s in x.shape)
+    k = kernel.detach()
+    if k.dtype not in (torch.float32, torch.float64):
+        k = k.float()
+    kshape = tuple(kernel.shape)
+    k = k.reshape(k.shape[0], k.shape[1], -1).contiguous()
+    O, K = int(k.shape[0]), int(k.shape[2])
+    g = gy.detach().to(k.dtype).contiguous()
+    dx = torch.empty_like(x) if need_x else None
+    dk = torch.empty((O, int(k.shape[1]), K), dtype=k.dtype, device=x.device) if need_k else None
+    db = (torch.empty((O,), dtype=k.dtype, device=x.device)
+          if (need_b and bias is not None) else None)
+    pm = _abi.PAD_MODES.get(cfg["padding_mode"])
+    if pm is None:
+        raise ValueError(f"unsupported padding_mode {cfg['padding_mode']!r}")
+    st = _abi.lib().hg_hexconv2d_backward(
+        _abi.ptr(x), _abi.ptr(k), _abi.ptr(g), _abi.ptr(dx), _abi.ptr(dk), _abi.ptr(db),
+        _abi.dtype_code(x.dtype), _abi.dtype_code(k.dtype), B, C, O, h, w, cfg["r"],
+        cfg["stride"], cfg["pad"], cfg["dilation"], cfg["groups"], int(cfg["off"]), pm,
+        float(cfg["padding_value"]), _abi.stream_of(x))
+    _abi.check(st, "hg_hexconv2d_backward")
+    gk = dk.reshape(kshape).to(kernel.dtype) if dk is not None else None
+    gb = db.to(bias.dtype) if db is not None else None
+    return dx, gk, gb
 
 
 HG_EUNSUP = -4

@@ -19,6 +19,7 @@
 #include <climits>
 
 #include "common.h"
+#include "hexconv_geom.h"
 
 namespace hg {
 
@@ -40,45 +41,6 @@ struct ConvGeom {
     int mink;         // min column tap offset over both parities
     double pad_value;
 };
-
-__host__ __device__ inline int64_t pad_map(int64_t i, int64_t n, int mode) {
-    if (i >= 0 && i < n) return i;
-    switch (mode) {
-    case HG_PAD_REFLECT:
-        while (i < 0 || i >= n) { if (i < 0) i = -i; if (i >= n) i = 2 * (n - 1) - i; }
-        return i;
-    case HG_PAD_REPLICATE:
-        return i < 0 ? 0 : n - 1;
-    case HG_PAD_CIRCULAR:
-        return ((i % n) + n) % n;
-    default:
-        return -1;
-    }
-}
-
-// Tap table in kernel-flattening order (HexFrames.py:114-118).
-__host__ __device__ inline void tap_geom(int r, int s, int d, int op, int t, int* dy, int* dk0,
-                                         int* dk1) {
-    int n = 0;
-    for (int ii = 0; ii < 2 * r - 1; ++ii) {
-        int tt = ii - r + 1;
-        tt = tt < 0 ? -tt : tt;
-        const int ln = 2 * r - 1 - tt;
-        if (t < n + ln) {
-            const int m = t - n;
-            const int col = tt * d + 2 * d * m;
-            *dy = ii * d;
-            for (int par = 0; par < 2; ++par) {
-                const int y = par * s + ii * d;
-                const int L = ((y & 1) + op) & 1;
-                const int dk = (1 + par * s + col - L) >> 1;
-                if (par == 0) *dk0 = dk; else *dk1 = dk;
-            }
-            return;
-        }
-        n += ln;
-    }
-}
 
 template <typename Tin, typename Tout, typename A, int OCB, int KFIX>
 __global__ __launch_bounds__(CV_THREADS) void k_hexconv(const Tin* __restrict__ x,
@@ -229,18 +191,6 @@ __global__ __launch_bounds__(256) void k_hexconv_direct(const Tin* __restrict__ 
     y[idx] = from_acc<Tout>(acc);
 }
 
-static int conv_out_shape(int64_t h, int64_t w, int r, int s, int p, int d, int64_t* ho,
-                          int64_t* wo) {
-    if (r < 1 || s < 1 || d < 1 || p < 0 || h < 0 || w < 0) return HG_EINVAL;
-    const int64_t kh = (int64_t)(2 * r - 2) * d + 1;
-    const int64_t kw = (int64_t)2 * d * (2 * r - 2) + 1;
-    const int64_t H = h + 2 * p, W = w + 2 * p;
-    if (H < kh || 2 * W - s < kw) return HG_ESHAPE;
-    *ho = (H - kh) / s + 1;
-    *wo = (2 * W - s - kw) / (2 * s) + 1;
-    return HG_OK;
-}
-
 template <typename Tin, typename Tout, typename A, int OCB, int KFIX>
 static int launch_conv(const void* x, const void* k, const void* b, void* y, ConvGeom G,
                        hipStream_t st) {
@@ -303,13 +253,8 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
     ConvGeom G;
     int st = conv_out_shape(h, w, radius, stride, padding, dilation, &G.ho, &G.wo);
     if (st) return st;
-    if (batch < 0 || in_channels < 1 || out_channels < 1 || groups < 1) return HG_EINVAL;
-    if (in_channels % groups || out_channels % groups) return HG_EINVAL;
-    if (pad_mode < HG_PAD_CONSTANT || pad_mode > HG_PAD_CIRCULAR) return HG_EINVAL;
-    if (pad_mode == HG_PAD_REFLECT && padding > 0 && (padding >= h || padding >= w))
-        return HG_ESHAPE;
-    if (pad_mode != HG_PAD_CONSTANT && padding > 0 && (h == 0 || w == 0)) return HG_ESHAPE;
-    if (pad_mode == HG_PAD_CIRCULAR && (padding > h || padding > w)) return HG_ESHAPE;
+    st = conv_check_args(batch, in_channels, out_channels, h, w, groups, padding, pad_mode);
+    if (st) return st;
     G.K = 3 * radius * radius - 3 * radius + 1;
     if (G.K > CV_MAXK) return HG_EUNSUP;
     if (batch == 0 || G.ho == 0 || G.wo == 0) return HG_OK;

@@ -106,6 +106,21 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
                  int padding, int dilation, int groups, int even_odd_offset, int pad_mode,
                  double pad_value, void* stream);
 
+/* HexConv2d backward: gradients of hg_hexconv2d for an upstream gradient gy
+ * (B, O, ho, wo) of w_dtype.  Replaces the reference's autograd path through
+ * HexConv2d.forward (HexFrames.py:96-169: pad -> heximage_to_type1 -> two strided
+ * F.conv2d -> interleave); computed as the exact adjoint of the forward index map.
+ * dx: (B, C, h, w) of x_dtype (float), or NULL; dkernel: (O, C/groups, K) of
+ * w_dtype, or NULL; dbias: (O,) of w_dtype, or NULL.  Outputs are overwritten.
+ * x is read only for dkernel, kernel only for dx.  d kernel / d bias are sums
+ * over B*ho*wo samples accumulated with float atomics (run-to-run last-bit
+ * differences, as torch's own conv weight gradients). */
+int hg_hexconv2d_backward(const void* x, const void* kernel, const void* gy, void* dx,
+                          void* dkernel, void* dbias, int x_dtype, int w_dtype, int64_t batch,
+                          int64_t in_channels, int64_t out_channels, int64_t h, int64_t w,
+                          int radius, int stride, int padding, int dilation, int groups,
+                          int even_odd_offset, int pad_mode, double pad_value, void* stream);
+
 /* Fused rect -> hex -> HexConv2d -> hex -> rect pass over a batch.
  * Replaces the chain rect_to_hex_resample(x, (h1,w1), 'bilinear')
  * (geometry_np.py:358-519) -> HexConv2d(C, O, even_odd_offset, 2, stride=1,

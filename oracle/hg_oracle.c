@@ -374,6 +374,69 @@ int or_hexconv2d(const double* x, const double* kern, const double* bias, double
     return 0;
 }
 
+/* HexConv2d backward: the exact adjoint of or_hexconv2d's index map (the reference
+ * gets it from torch autograd through pad -> heximage_to_type1 -> two strided
+ * F.conv2d -> interleave, HexFrames.py:96-169).  For every output sample and tap
+ * the forward reads one padded sample P[yy][k]; its input pixel (after the padding
+ * mode's index map, pad_index) receives kern*gy, the tap's weight receives
+ * gy*value, the bias receives gy.  Constant-mode padding samples have no input
+ * pixel (their value is the constant).  Serial in (b, o) so the accumulation order
+ * is fixed.  dx / dk / db may be NULL; they are overwritten (not accumulated). */
+int or_hexconv2d_backward(const double* x, const double* kern, const double* gy, double* dx,
+                          double* dk, double* db, int64_t B, int64_t C, int64_t O, int64_t h,
+                          int64_t w, int r, int s, int p, int d, int groups, int off,
+                          int pad_mode, double pad_value) {
+    int64_t ho, wo;
+    int st = or_hexconv2d_out_shape(h, w, r, s, p, d, &ho, &wo);
+    if (st) return st;
+    if (groups < 1 || C % groups || O % groups) return -1;
+    int K = 3 * r * r - 3 * r + 1;
+    int64_t cg = C / groups, og = O / groups;
+    int64_t Wp = w + 2 * p;
+    int op = (off + p) % 2;
+    int* tii = (int*)malloc(sizeof(int) * K);
+    int* tcol = (int*)malloc(sizeof(int) * K);
+    int n = 0;
+    for (int ii = 0; ii < 2 * r - 1; ++ii) {
+        int t = abs(ii - r + 1), ln = 2 * r - 1 - t;
+        for (int m = 0; m < ln; ++m) { tii[n] = ii; tcol[n] = t * d + 2 * d * m; ++n; }
+    }
+    if (dx) memset(dx, 0, sizeof(double) * (size_t)(B * C * h * w));
+    if (dk) memset(dk, 0, sizeof(double) * (size_t)(O * cg * K));
+    if (db) memset(db, 0, sizeof(double) * (size_t)O);
+    for (int64_t b = 0; b < B; ++b)
+        for (int64_t o = 0; o < O; ++o) {
+            int64_t g = o / og;
+            for (int64_t ro = 0; ro < ho; ++ro)
+                for (int64_t q = 0; q < wo; ++q) {
+                    double gv = gy[((b * O + o) * ho + ro) * wo + q];
+                    if (db) db[o] += gv;
+                    for (int64_t ci = 0; ci < cg; ++ci) {
+                        int64_t c = g * cg + ci;
+                        const double* xin = x + (b * C + c) * h * w;
+                        for (int t = 0; t < K; ++t) {
+                            int64_t yy = s * ro + (int64_t)tii[t] * d;
+                            int64_t xx = 1 + ((ro & 1) ? s : 0) + 2 * s * q + tcol[t];
+                            int64_t L = ((yy & 1) + op) & 1;
+                            int64_t u = xx - L;
+                            if (u > 2 * Wp - 1) continue;      /* type1 structural zero */
+                            int64_t k = u >> 1;
+                            int64_t ry = pad_index(yy - p, h, pad_mode);
+                            int64_t rx = pad_index(k - p, w, pad_mode);
+                            int inside = !(pad_mode == OR_PAD_CONSTANT && (ry < 0 || rx < 0));
+                            double v = inside ? xin[ry * w + rx] : pad_value;
+                            if (dk) dk[(o * cg + ci) * K + t] += gv * v;
+                            if (dx && inside)
+                                dx[(b * C + c) * h * w + ry * w + rx] += kern[(o * cg + ci) * K + t] * gv;
+                        }
+                    }
+                }
+        }
+    free(tii);
+    free(tcol);
+    return 0;
+}
+
 /* heximage_to_type1 (HexFrames.py:417-445): (planes,h,w) -> (planes,h,2w+1) */
 void or_heximage_to_type1(const double* x, double* t, int64_t planes, int64_t h, int64_t w,
                           int off) {

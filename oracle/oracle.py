@@ -11,6 +11,7 @@ Each function mirrors one reference entry point (paths under /root/reference):
                 HyGrid/geometry_torch.py:335-347
   hexresize     HyGrid/geometry_np.py:520-681
   hexconv2d     HyGrid/HexFrames.py:96-169
+  hexconv2d_backward  the adjoint of hexconv2d (reference: torch autograd of :96-169)
 Inputs are (planes, h, w) arrays of any real dtype; outputs are float64.
 """
 import ctypes
@@ -51,6 +52,8 @@ def lib():
         L.or_hexconv2d_out_shape.argtypes = [_i64, _i64] + [ctypes.c_int] * 4 + [
             ctypes.POINTER(_i64), ctypes.POINTER(_i64)]
         L.or_hexconv2d.argtypes = [_dp, _dp, _dp, _dp] + [_i64] * 5 + [ctypes.c_int] * 7 + [
+            ctypes.c_double]
+        L.or_hexconv2d_backward.argtypes = [_dp] * 6 + [_i64] * 5 + [ctypes.c_int] * 7 + [
             ctypes.c_double]
         L.or_heximage_to_type1.argtypes = [_dp, _dp, _i64, _i64, _i64, ctypes.c_int]
         L.or_heximage_to_type1.restype = None
@@ -157,6 +160,28 @@ def hexconv2d(x, kernel, bias, even_odd_offset, radius, stride=1, padding=0, dil
     if st:
         raise ValueError(f"hexconv2d oracle status {st}")
     return y
+
+
+def hexconv2d_backward(x, kernel, gy, even_odd_offset, radius, stride=1, padding=0,
+                       dilation=1, groups=1, padding_mode="constant", padding_value=0.0):
+    """(dx, dkernel, dbias) of hexconv2d for upstream gradient gy (all float64)."""
+    x = np.ascontiguousarray(x, np.float64)
+    while x.ndim < 4:
+        x = x[None]
+    B, C, h, w = x.shape
+    k = np.ascontiguousarray(kernel, np.float64)
+    O = k.shape[0]
+    gy = np.ascontiguousarray(gy, np.float64)
+    dx = np.empty_like(x)
+    dk = np.empty_like(k)
+    db = np.empty((O,), np.float64)
+    st = lib().or_hexconv2d_backward(_dptr(x), _dptr(k), _dptr(gy), _dptr(dx), _dptr(dk),
+                                     _dptr(db), B, C, O, h, w, radius, stride, padding,
+                                     dilation, groups, int(even_odd_offset),
+                                     PAD_MODES[padding_mode], float(padding_value))
+    if st:
+        raise ValueError(f"hexconv2d_backward oracle status {st}")
+    return dx, dk, db
 
 
 def heximage_to_type1(x, even_odd_offset):

@@ -290,6 +290,40 @@ def gen_conv():
     return arrs, index
 
 
+def gen_conv_bwd():
+    """HexConv2d gradients from the reference's own autograd graph (pad -> type1 ->
+    two strided F.conv2d -> interleave, HexFrames.py:96-169) for a seeded upstream
+    gradient: d input, d kernel, d bias of every forward case above."""
+    arrs, index = {}, []
+    for ci, p in enumerate(conv_cases()):
+        torch.manual_seed(1000 + ci)
+        p = dict(p)
+        in_c = p.setdefault("in_c", 3)
+        try:
+            m = HF.HexConv2d(in_c, p["out_c"], p["off"], p["r"], stride=p["stride"],
+                             padding=p["pad"], dilation=p["dilation"], groups=p["groups"],
+                             bias=p["bias"], padding_mode=p["padding_mode"],
+                             padding_value=p["padding_value"])
+            x = torch.rand(2, in_c, p["h"], p["w"]).requires_grad_(True)
+            y = m(x)
+            g = torch.Generator().manual_seed(5000 + ci)
+            gy = torch.randn(y.shape, generator=g)
+            y.backward(gy)
+        except Exception as e:  # configurations the reference itself rejects
+            index.append(dict(case=ci, **p, error=type(e).__name__))
+            continue
+        arrs[f"c{ci}_x"] = x.detach().numpy()
+        arrs[f"c{ci}_kernel"] = m.kernel.detach().numpy()
+        if m.bias is not None:
+            arrs[f"c{ci}_bias"] = m.bias.detach().numpy()
+            arrs[f"c{ci}_dbias"] = m.bias.grad.numpy()
+        arrs[f"c{ci}_gy"] = gy.numpy()
+        arrs[f"c{ci}_dx"] = x.grad.numpy()
+        arrs[f"c{ci}_dkernel"] = m.kernel.grad.numpy()
+        index.append(dict(case=ci, **p, out_shape=list(y.shape)))
+    return arrs, index
+
+
 def gen_taps():
     """Impulse tap tables: output (r,q) of tap t reads input flat index table[t,r,q] (-1: zero)."""
     arrs, index = {}, []
@@ -373,7 +407,7 @@ def main():
     meta = {"reference": REF, "numpy": np.__version__, "torch": torch.__version__}
     for name, fn in (("r2h", lambda: gen_r2h(rng)), ("h2r", lambda: gen_h2r(rng, gt)),
                      ("hexresize", lambda: gen_resize(rng)), ("hexconv", gen_conv),
-                     ("taps", gen_taps)):
+                     ("hexconv_bwd", gen_conv_bwd), ("taps", gen_taps)):
         arrs, index = fn()
         np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arrs)
         meta[name] = index

@@ -97,6 +97,30 @@ def test_hexconv_all_cases(golden, golden_index):
     assert n >= 50
 
 
+def test_hexconv_backward_all_cases(golden, golden_index):
+    """Oracle adjoint vs the reference's own autograd gradients (d input, d kernel,
+    d bias) for every forward case; the reference computes them in fp32."""
+    g = golden("hexconv_bwd")
+    n = 0
+    for meta in golden_index["hexconv_bwd"]:
+        if "error" in meta:
+            continue
+        ci = meta["case"]
+        dx, dk, db = O.hexconv2d_backward(
+            g[f"c{ci}_x"], g[f"c{ci}_kernel"], g[f"c{ci}_gy"], meta["off"], meta["r"],
+            meta["stride"], meta["pad"], meta["dilation"], meta["groups"],
+            meta["padding_mode"], meta["padding_value"])
+        for got, key in ((dx, "dx"), (dk, "dkernel")):
+            ref = g[f"c{ci}_{key}"]
+            assert got.shape == ref.shape, (ci, key, got.shape, ref.shape)
+            np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-5 * max(np.abs(ref).max(), 1),
+                                       err_msg=f"{key} {meta}")
+        if f"c{ci}_dbias" in g:
+            np.testing.assert_allclose(db, g[f"c{ci}_dbias"], rtol=1e-4, atol=1e-4)
+        n += 1
+    assert n >= 50
+
+
 def test_conv_impulse_tap_tables(golden, golden_index):
     g = golden("taps")
     for meta in golden_index["taps"]:
