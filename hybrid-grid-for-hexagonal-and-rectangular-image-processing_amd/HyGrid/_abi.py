@@ -38,6 +38,7 @@ SIGNATURES = {
     "hg_rect_to_hex": _RESAMPLE,
     "hg_hex_to_rect": _RESAMPLE,
     "hg_hexresize": _RESAMPLE,
+    "hg_resample_backward": ([_int, _vp, _vp, _int] + [_i64] * 5 + [_int, _vp], _int),
     "hg_lattice_maps": ([_int, _i64, _i64, _i64, _i64, _vp, _vp, _vp], _int),
     "hg_hexconv2d_out_shape": ([_i64, _i64, _int, _int, _int, _int,
                                 ctypes.POINTER(_i64), ctypes.POINTER(_i64)], _int),

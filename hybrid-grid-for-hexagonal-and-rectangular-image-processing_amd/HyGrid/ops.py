@@ -28,8 +28,45 @@ def _planes(x):
     return x, lead, planes
 
 
+_RESAMPLE_OP = {"hg_rect_to_hex": _abi.HG_OP_RECT_TO_HEX, "hg_hex_to_rect": _abi.HG_OP_HEX_TO_RECT,
+                "hg_hexresize": _abi.HG_OP_HEXRESIZE}
+
+
+class _ResampleFn(torch.autograd.Function):
+    """Autograd of a resample: backward = hg_resample_backward (the transpose of the
+    forward's lattice weights)."""
+
+    @staticmethod
+    def forward(ctx, x, fn_name, size, interp, out_dtype):
+        ctx.meta = (_RESAMPLE_OP[fn_name], tuple(x.shape), x.dtype, int(interp))
+        return _resample_raw(fn_name, x, size, interp, out_dtype)
+
+    @staticmethod
+    def backward(ctx, gy):
+        op, shape, xdt, interp = ctx.meta
+        acc = torch.float64 if torch.float64 in (gy.dtype, xdt) else torch.float32
+        g = gy.contiguous().to(acc)
+        h, w = shape[-2], shape[-1]
+        h1, w1 = int(g.shape[-2]), int(g.shape[-1])
+        planes = 1
+        for d in shape[:-2]:
+            planes *= d
+        dx = torch.empty(shape, dtype=acc, device=gy.device)
+        st = _abi.lib().hg_resample_backward(op, _abi.ptr(g), _abi.ptr(dx), _abi.dtype_code(acc),
+                                             planes, h, w, h1, w1, interp, _abi.stream_of(g))
+        _abi.check(st, "hg_resample_backward")
+        return dx.to(xdt), None, None, None, None
+
+
 def _resample(fn_name, x, size, interp, out_dtype):
+    if torch.is_grad_enabled() and x.requires_grad and x.is_floating_point():
+        return _ResampleFn.apply(x, fn_name, size, interp, out_dtype)
+    return _resample_raw(fn_name, x, size, interp, out_dtype)
+
+
+def _resample_raw(fn_name, x, size, interp, out_dtype):
     _abi.require_device(x)
+    x = x.detach()
     x, lead, planes = _planes(x)
     h, w = int(x.shape[-2]), int(x.shape[-1])
     h1, w1 = (h, w) if size is None else (int(size[0]), int(size[1]))

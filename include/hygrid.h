@@ -78,6 +78,16 @@ int hg_hex_to_rect(const void* src, void* dst, int src_dtype, int dst_dtype, int
 int hg_hexresize(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t planes,
                  int64_t h, int64_t w, int64_t h1, int64_t w1, int interp, void* stream);
 
+/* Gradient of a resample: d src (planes, h, w) of acc_dtype (F32 or F64) for an
+ * upstream gradient gy (planes, h1, w1) of acc_dtype.  op: HG_OP_RECT_TO_HEX /
+ * HG_OP_HEX_TO_RECT / HG_OP_HEXRESIZE with the forward's interp.  Replaces torch
+ * autograd through geometry_torch's gathers and blends (geometry_torch.py:290-358);
+ * the transpose of the forward's lattice weights (geometry_np.py:514-517 bilinear,
+ * :347-354 triangle, nearest = the chosen neighbour).  dx is overwritten; the
+ * scatter uses float atomics (last-bit run-to-run differences). */
+int hg_resample_backward(int op, const void* gy, void* dx, int acc_dtype, int64_t planes,
+                         int64_t h, int64_t w, int64_t h1, int64_t w1, int interp, void* stream);
+
 /* Integer lattice maps (and fp64 coefficients) of one resample, for parity tests.
  * imaps: int32 [5][h1][w1] = i_n, j_n, up_down_flag, valid bitmask (bit k-1 =
  *        valid_indices_k), nearest argmin — the locals of the reference function
