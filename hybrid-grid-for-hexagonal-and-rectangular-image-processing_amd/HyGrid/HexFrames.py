@@ -135,29 +135,23 @@ class HexConv2d(nn.Module):
 
 # -------------------------- format conversion -------------------------------
 def heximage_to_type1(input: torch.Tensor, even_odd_offset) -> torch.Tensor:
-    """Offset-row hex image -> double-width type1 raster (HexFrames.py:417-445).
-
+    """Offset-row hex image -> double-width type1 raster (HexFrames.py:417-445), one
+    gfx950 permute (hg_hex_to_type1):
     type1[y, 2k+L(y)] = type1[y, 2k+1+L(y)] = x[y, k], L(y) = (y%2 + off)%2, 0 elsewhere.
-    """
+    Output dtype: torch's default float dtype, as the reference's torch.empty (:439)."""
     while input.dim() < 4:
         input = input.unsqueeze(0)
-    B, C, H, W = input.shape
-    out = torch.zeros((B, C, H, 2 * W + 1), dtype=torch.get_default_dtype(),
-                      device=input.device)
-    for par in (0, 1):
-        L = (par + even_odd_offset) % 2
-        rows = input[:, :, par::2, :].to(out.dtype)
-        out[:, :, par::2, L:L + 2 * W:2] = rows
-        out[:, :, par::2, L + 1:L + 2 * W:2] = rows
-    return out
+    return ops.hex_to_type1(input, even_odd_offset, 1, torch.get_default_dtype())
 
 
 def heximage_to_type2(input: torch.Tensor, even_odd_offset) -> torch.Tensor:
     """type1 with every row doubled (HexFrames.py:446-449)."""
-    return heximage_to_type1(input, even_odd_offset).repeat_interleave(2, dim=2)
+    while input.dim() < 4:
+        input = input.unsqueeze(0)
+    return ops.hex_to_type1(input, even_odd_offset, 2, torch.get_default_dtype())
 
 
 def type1_to_heximage(input: torch.Tensor, even_odd_offset: int):
-    """type1 -> hex image (HexFrames.py:450-458): columns 1::2, offset passed through."""
+    """type1 -> hex image (HexFrames.py:450-458): columns 1::2 (a view, as the
+    reference's slice), offset passed through."""
     return input[:, :, :, 1::2], even_odd_offset
-

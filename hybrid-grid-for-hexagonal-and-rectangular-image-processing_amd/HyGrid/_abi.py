@@ -46,6 +46,8 @@ SIGNATURES = {
                       _int, _int, _int, _int, _int, _int, _int, _dbl, _vp], _int),
     "hg_hexconv2d_backward": ([_vp] * 6 + [_int, _int] + [_i64] * 5 + [_int] * 7 + [_dbl, _vp],
                               _int),
+    "hg_hex_to_type1": ([_vp, _vp, _int] + [_i64] * 3 + [_int, _int, _vp], _int),
+    "hg_strided_copy2d": ([_vp, _vp, _int] + [_i64] * 9 + [_vp], _int),
     "hg_pipeline_r2h_conv_h2r": ([_vp, _vp, _vp, _vp, _int, _int] + [_i64] * 9 +
                                  [_int, _int, _int, _dbl, _vp], _int),
 }

@@ -201,6 +201,42 @@ def hexconv2d_backward(gy, x, kernel, bias, cfg, need_x=True, need_k=True, need_
     return dx, gk, gb
 
 
+def hex_to_type1(x, even_odd_offset, row_repeat=1, out_dtype=None):
+    """Offset-row hex raster (..., H, W) -> type1 (..., H*row_repeat, 2W+1) on the GPU
+    (hg_hex_to_type1): row_repeat 1 = HexFrames.heximage_to_type1 (HexFrames.py:417-445),
+    2 = heximage_to_type2 (:446-449).  out_dtype converts first (the reference's torch
+    version returns the default float dtype)."""
+    _abi.require_device(x)
+    if out_dtype is not None and x.dtype != out_dtype:
+        x = x.to(out_dtype)
+    x, lead, planes = _planes(x)
+    h, w = int(x.shape[-2]), int(x.shape[-1])
+    y = torch.empty(lead + (h * row_repeat, 2 * w + 1), dtype=x.dtype, device=x.device)
+    st = _abi.lib().hg_hex_to_type1(_abi.ptr(x), _abi.ptr(y), x.element_size(), planes, h, w,
+                                    int(even_odd_offset) & 1, int(row_repeat), _abi.stream_of(x))
+    _abi.check(st, "hg_hex_to_type1")
+    return y
+
+
+def strided_copy2d(x, row_start, row_step, col_start, col_step, h_out=None, w_out=None):
+    """Contiguous x[..., row_start::row_step, col_start::col_step] (bounded by h_out /
+    w_out) by one gfx950 gather (hg_strided_copy2d): type1 / type2 decoding
+    (HexImage.py:108-111, HexFrames.py:450-458) into a kernel-ready raster."""
+    _abi.require_device(x)
+    x, lead, planes = _planes(x)
+    H, W = int(x.shape[-2]), int(x.shape[-1])
+    if h_out is None:
+        h_out = len(range(row_start, H, row_step))
+    if w_out is None:
+        w_out = len(range(col_start, W, col_step))
+    y = torch.empty(lead + (h_out, w_out), dtype=x.dtype, device=x.device)
+    st = _abi.lib().hg_strided_copy2d(_abi.ptr(x), _abi.ptr(y), x.element_size(), planes, H, W,
+                                      row_start, row_step, col_start, col_step, h_out, w_out,
+                                      _abi.stream_of(x))
+    _abi.check(st, "hg_strided_copy2d")
+    return y
+
+
 HG_EUNSUP = -4
 
 

@@ -131,6 +131,20 @@ int hg_hexconv2d_backward(const void* x, const void* kernel, const void* gy, voi
                           int radius, int stride, int padding, int dilation, int groups,
                           int even_odd_offset, int pad_mode, double pad_value, void* stream);
 
+/* Hex raster storage formats (pure memory permutes; any element size 1/2/4/8).
+ * hg_hex_to_type1: (planes, h, w) offset-row hex image -> (planes, h*row_repeat, 2w+1)
+ * "type1" double-width raster T[y][2k+L] = T[y][2k+1+L] = x[y][k], L = (y%2+off)%2,
+ * zeros elsewhere; row_repeat 1 replaces HexFrames.heximage_to_type1
+ * (HexFrames.py:417-445) / HEXIMAGE.GenerateType1Image (HexImage.py:139-153),
+ * row_repeat 2 the type2 raster (HexFrames.py:446-449, HexImage.py:154-170).
+ * hg_strided_copy2d: dst[p][i][j] = src[p][row_start + i*row_step][col_start + j*col_step]
+ * (contiguous decode of type1 / type2 rasters, HexImage.py:108-111, HexFrames.py:450-458). */
+int hg_hex_to_type1(const void* src, void* dst, int elem_size, int64_t planes, int64_t h,
+                    int64_t w, int even_odd_offset, int row_repeat, void* stream);
+int hg_strided_copy2d(const void* src, void* dst, int elem_size, int64_t planes, int64_t H,
+                      int64_t W, int64_t row_start, int64_t row_step, int64_t col_start,
+                      int64_t col_step, int64_t h_out, int64_t w_out, void* stream);
+
 /* Fused rect -> hex -> HexConv2d -> hex -> rect pass over a batch.
  * Replaces the chain rect_to_hex_resample(x, (h1,w1), 'bilinear')
  * (geometry_np.py:358-519) -> HexConv2d(C, O, even_odd_offset, 2, stride=1,
