@@ -16,7 +16,10 @@ Departures (documented in DESIGN.md):
 * hex_to_rect_resample(..., 'nearest') and hexresize(..., 'nearest') work,
   with geometry_torch's rule (geometry_torch.py:335-347) — the NumPy reference
   raises ValueError there (:339, :664);
-* hex_to_rect_resample(..., 'bilinear') raises ValueError — the reference runs
+* image_geometric_transformation(..., 'nearest') works with geometry_torch's rule
+  (geometry_torch.py:165-173); the NumPy reference raises ValueError (:172);
+* hex_to_rect_resample / image_geometric_transformation(..., 'bilinear') raise
+  ValueError — the reference runs
   no blend and returns the uninitialised np.empty (:268-272, :356).
 """
 import numpy as np
@@ -24,7 +27,8 @@ import torch
 
 from . import _abi, ops
 
-__all__ = ["rect_to_hex_resample", "hex_to_rect_resample", "hexresize"]
+__all__ = ["image_geometric_transformation", "rect_to_hex_resample", "hex_to_rect_resample",
+           "hexresize"]
 
 _NP_TO_TORCH = {
     np.dtype(np.uint8): torch.uint8, np.dtype(np.int8): torch.int8,
@@ -104,3 +108,21 @@ def hexresize(image, dsize, interpolation="linear", offset=0, *, out_dtype=None,
         raise ValueError(f"hexresize: interpolation must be 'linear' or 'nearest', "
                          f"got {interpolation!r}")
     return _run(ops.hexresize, image, dsize, method, out_dtype, squeeze)
+
+
+def image_geometric_transformation(img, H=np.eye(3), interpolation='nearest', offset=0,
+                                   *, out_dtype=None, squeeze=True):
+    """Affine transform of a hex raster onto a new hex lattice; reference
+    geometry_np.py:6-189.  The output lattice spans the transformed corners of the
+    input (:56-87), each sample is inverse-mapped by inv(H) and blended from its
+    triangle of input hexagons (:104-187).  `offset` is dead in the reference and
+    ignored here."""
+    method_dict = {'nearest': 0, 'linear': 1, 'bilinear': 2}
+    method = method_dict[interpolation]          # KeyError, as the reference (:17)
+    if method == 2:
+        raise ValueError("image_geometric_transformation: 'bilinear' has no blend in the "
+                         "reference (it returns np.empty, geometry_np.py:103-189); use 'linear'")
+    if img.ndim not in (2, 3, 4):
+        raise Exception(f"dim of image should be 2 or 3, but got dim = {img.ndim} instead")
+    return _run(lambda x, size, interp, od: ops.hex_homography(x, H, interp, od),
+                img, None, method, out_dtype, squeeze)

@@ -117,6 +117,81 @@ def lattice_maps(op, h, w, h1, w1, device=None):
     return out
 
 
+def homography_plan(h, w, H):
+    """Host planning of image_geometric_transformation (geometry_np.py:56-102): the
+    output axes of the transformed corners and inv(H), in NumPy exactly as the
+    reference computes them (O(h1 + w1) work).  Returns (xs, ys, hinv) as float64
+    ndarrays; h1 = len(xs), w1 = len(ys)."""
+    import numpy as np
+    H = np.asarray(H.detach().cpu() if isinstance(H, torch.Tensor) else H, dtype=np.float64)
+    if H.shape != (3, 3):
+        raise ValueError(f"H must be 3x3, got shape {H.shape}")
+    corner = np.array([[-(h / 2 - 0.5), -((w + 0.5) / 2 - 0.5), 1.],
+                       [-(h / 2 - 0.5), (w + 0.5) / 2 - 0.5, 1.],
+                       [h / 2 - 0.5, -((w + 0.5) / 2 - 0.5), 1.],
+                       [h / 2 - 0.5, (w + 0.5) / 2 - 0.5, 1.]]).transpose()
+    c = np.matmul(H, corner)
+    h1_inf, w1_inf = np.min(c[0], axis=-1), np.min(c[1], axis=-1)
+    h1_sup, w1_sup = np.max(c[0], axis=-1), np.max(c[1], axis=-1)
+    xs = np.arange(h1_inf, h1_sup + 1, 1).astype(np.float64)
+    ys = np.arange(w1_inf, w1_sup + 0.5, 1).astype(np.float64)
+    hinv = np.ascontiguousarray(np.linalg.inv(H), dtype=np.float64)
+    return xs, ys, hinv
+
+
+def _homography_args(x, H):
+    import numpy as np
+    h, w = int(x.shape[-2]), int(x.shape[-1])
+    xs, ys, hinv = homography_plan(h, w, H)
+    dxs = torch.from_numpy(xs).to(x.device)
+    dys = torch.from_numpy(ys).to(x.device)
+    return h, w, dxs, dys, hinv.ctypes.data_as(ctypes.c_void_p), hinv
+
+
+def hex_homography(x, H, interp=_abi.HG_LINEAR, out_dtype=None):
+    """hex (..., H, W) -> hex (..., h1, w1) under the affine map H
+    (image_geometric_transformation, geometry_np.py:6-189), by hg_hex_homography.
+    'linear' blends in fp64 and returns out_dtype (default: x's float dtype, float32 for
+    integer input); 'nearest' copies the first-minimum vertex (geometry_torch.py:165-173)."""
+    _abi.require_device(x)
+    x = x.detach()
+    x, lead, planes = _planes(x)
+    h, w, dxs, dys, hptr, _keep = _homography_args(x, H)
+    h1, w1 = int(dxs.numel()), int(dys.numel())
+    if interp == _abi.HG_NEAREST:
+        out_dtype = x.dtype
+    elif out_dtype is None:
+        out_dtype = x.dtype if x.dtype in _FLOATS else torch.float32
+    y = torch.empty(lead + (h1, w1), dtype=out_dtype, device=x.device)
+    st = _abi.lib().hg_hex_homography(
+        _abi.ptr(x), _abi.ptr(y), _abi.dtype_code(x.dtype), _abi.dtype_code(out_dtype),
+        planes, h, w, h1, w1, _abi.ptr(dxs), _abi.ptr(dys), hptr, int(interp),
+        _abi.stream_of(x))
+    _abi.check(st, "hg_hex_homography")
+    return y
+
+
+def homography_maps(h, w, H, device=None):
+    """Lattice maps of one image_geometric_transformation (parity tests): the keys of
+    lattice_maps plus the inverse-mapped point x_, y_ (geometry_np.py:104-105)."""
+    device = torch.device("cuda") if device is None else torch.device(device)
+    if not torch.cuda.is_available():
+        raise RuntimeError("HyGrid needs a HIP device (MI355X); none is available.")
+    probe = torch.empty((h, w), device=device)
+    h, w, dxs, dys, hptr, _keep = _homography_args(probe, H)
+    h1, w1 = int(dxs.numel()), int(dys.numel())
+    im = torch.empty((5, h1, w1), dtype=torch.int32, device=device)
+    fm = torch.empty((7, h1, w1), dtype=torch.float64, device=device)
+    st = _abi.lib().hg_hex_homography_maps(h, w, h1, w1, _abi.ptr(dxs), _abi.ptr(dys), hptr,
+                                           _abi.ptr(im), _abi.ptr(fm), _abi.stream_of(im))
+    _abi.check(st, "hg_hex_homography_maps")
+    keys = ("i_n", "j_n", "flag", "valid", "argmin")
+    out = {k: im[i] for i, k in enumerate(keys)}
+    out.update({k: fm[i] for i, k in enumerate(("i_f", "j_f", "alpha", "beta", "gamma",
+                                                 "x_", "y_"))})
+    return out
+
+
 def hexconv2d_out_shape(h, w, radius, stride=1, padding=0, dilation=1):
     ho, wo = ctypes.c_int64(), ctypes.c_int64()
     st = _abi.lib().hg_hexconv2d_out_shape(h, w, radius, stride, padding, dilation,

@@ -109,10 +109,13 @@ struct TriSample {
     double i_f, j_f, alpha, beta, gamma;
 };
 
-__host__ __device__ __forceinline__ TriSample tri_sample(const Geom& g, int64_t a, int64_t b) {
+// The triangle sample at the Cartesian hex-frame point (x_, y_) of a source hex raster
+// (h, w) = (g.h, g.w).  Shared by hex->rect / hexresize (x_, y_ from linspace axes) and
+// image_geometric_transformation (x_, y_ from an inverse homography, geometry_np.py:107-187,
+// whose i_f = i_ - i_n equals the (float) cast below for |i_n| < 2^24).
+__host__ __device__ __forceinline__ TriSample tri_sample_xy(const Geom& g, double x_, double y_) {
     TriSample s;
     const double hh = g.hh, ww = g.ww;
-    double x_ = axis_at(g.xs, a), y_ = axis_at(g.ys, b);
     double i_ = x_ + (double)(g.h - 1) * 0.5;            // :276
     double j_ = 0.5 * i_ + y_ + (ww - 0.5) * 0.5;        // :277
     s.i_n = (int64_t)i_;
@@ -158,6 +161,10 @@ __host__ __device__ __forceinline__ TriSample tri_sample(const Geom& g, int64_t 
     s.beta = S2 / S;
     s.gamma = S3 / S;
     return s;
+}
+
+__host__ __device__ __forceinline__ TriSample tri_sample(const Geom& g, int64_t a, int64_t b) {
+    return tri_sample_xy(g, axis_at(g.xs, a), axis_at(g.ys, b));
 }
 
 }  // namespace hg

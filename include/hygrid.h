@@ -145,6 +145,23 @@ int hg_strided_copy2d(const void* src, void* dst, int elem_size, int64_t planes,
                       int64_t W, int64_t row_start, int64_t row_step, int64_t col_start,
                       int64_t col_step, int64_t h_out, int64_t w_out, void* stream);
 
+/* Affine transform of a hex raster onto a new hex lattice: replaces the per-sample work
+ * of image_geometric_transformation (geometry_np.py:6-189, geometry_torch.py:7-189).
+ * xs (h1) / ys (w1): DEVICE fp64 output axes, np.arange(h1_inf, h1_sup + 1, 1) and
+ * np.arange(w1_inf, w1_sup + 0.5, 1) of the transformed corners (:56-87); odd rows are
+ * shifted by +0.5 in the kernel (:87).  hinv: HOST fp64 3x3 row-major inv(H) (:97-102;
+ * its third row is unused, as in the reference).  interp HG_LINEAR: 3-vertex triangle
+ * blend in fp64, dst F64/F32/F16/BF16 (:175-184); HG_NEAREST: first-minimum vertex,
+ * dst_dtype == src_dtype (geometry_torch.py:165-173; the NumPy twin raises there).
+ * hg_hex_homography_maps: int32 [5][h1][w1] maps as hg_lattice_maps, fp64 [7][h1][w1]
+ * = i_f, j_f, alpha, beta, gamma, x_, y_ (parity tests). */
+int hg_hex_homography(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t planes,
+                      int64_t h, int64_t w, int64_t h1, int64_t w1, const double* xs,
+                      const double* ys, const double* hinv, int interp, void* stream);
+int hg_hex_homography_maps(int64_t h, int64_t w, int64_t h1, int64_t w1, const double* xs,
+                           const double* ys, const double* hinv, int32_t* imaps, double* fmaps,
+                           void* stream);
+
 /* Fused rect -> hex -> HexConv2d -> hex -> rect pass over a batch.
  * Replaces the chain rect_to_hex_resample(x, (h1,w1), 'bilinear')
  * (geometry_np.py:358-519) -> HexConv2d(C, O, even_odd_offset, 2, stride=1,

@@ -12,6 +12,8 @@ Each function mirrors one reference entry point (paths under /root/reference):
   hexresize     HyGrid/geometry_np.py:520-681
   hexconv2d     HyGrid/HexFrames.py:96-169
   hexconv2d_backward  the adjoint of hexconv2d (reference: torch autograd of :96-169)
+  image_geometric_transformation  HyGrid/geometry_np.py:6-189 (NumPy restatement;
+                nearest per HyGrid/geometry_torch.py:165-173)
 Inputs are (planes, h, w) arrays of any real dtype; outputs are float64.
 """
 import ctypes
@@ -190,3 +192,68 @@ def heximage_to_type1(x, even_odd_offset):
     t = np.empty((n, h, 2 * w + 1), np.float64)
     lib().or_heximage_to_type1(_dptr(planes), _dptr(t), n, h, w, int(even_odd_offset))
     return t.reshape(tuple(lead) + (h, 2 * w + 1))
+
+
+def image_geometric_transformation(x, H, interp=1):
+    """NumPy restatement of geometry_np.image_geometric_transformation (:6-189) on
+    (planes, h, w) input; returns (y (planes, h1, w1), maps dict).  Output lattice: the
+    arange axes of the transformed corners (:56-87, odd rows +0.5); each sample is mapped
+    by inv(H) (:97-102) and blended from its triangle of input hexagons (:107-187).
+    interp 1 = 'linear' (fp64), 0 = nearest (first minimum, geometry_torch.py:165-173)."""
+    planes, lead = _as_planes(x)
+    n, h, w = planes.shape
+    H = np.asarray(H, np.float64)
+    hx, wy = h / 2 - 0.5, (w + 0.5) / 2 - 0.5
+    corners = np.array([[-hx, -wy, 1.], [-hx, wy, 1.], [hx, -wy, 1.], [hx, wy, 1.]]).T
+    c = np.matmul(H, corners)
+    xs = np.arange(c[0].min(), c[0].max() + 1, 1)
+    ys = np.arange(c[1].min(), c[1].max() + 0.5, 1)
+    X = np.repeat(xs[:, None], ys.size, axis=1)
+    Y = np.repeat(ys[None, :], xs.size, axis=0)
+    Y[1::2] += 0.5
+    Hi = np.linalg.inv(H)
+    xm = (Hi[0, 0] * X + Hi[0, 1] * Y) + Hi[0, 2]
+    ym = (Hi[1, 0] * X + Hi[1, 1] * Y) + Hi[1, 2]
+    fi = xm + (h - 1) * 0.5
+    fj = 0.5 * fi + ym + (w - 0.5) * 0.5
+    i_n, j_n = fi.astype(np.int64), fj.astype(np.int64)
+    flag = (fi - i_n) > (fj - j_n)
+    half1 = ((i_n + 1) / 2).astype(np.int64)
+    half2 = ((i_n + 2) / 2).astype(np.int64)
+    # vertices: p1 = (i, j - half1); p2 = flag ? (i+1, j - half2) : (i, j+1 - half1);
+    # p3 = (i+1, j+1 - half2)
+    rows = [i_n, np.where(flag, i_n + 1, i_n), i_n + 1]
+    cols = [j_n - half1, np.where(flag, j_n - half2, j_n + 1 - half1), j_n + 1 - half2]
+    ok = [(r >= 0) & (r < h) & (q >= 0) & (q < w) for r, q in zip(rows, cols)]
+    f = flag.astype(np.float64)
+    cx = (h - 1) / 2
+    cy = (w - 0.5) / 2
+    px = [i_n - cx, (i_n + f) - cx, (i_n + 1) - cx]
+    py = [j_n - i_n / 2 - cy, (j_n + 1 - f) - (i_n + f) / 2 - cy, (j_n + 1) - (i_n + 1) / 2 - cy]
+    dx = [xm - p for p in px]
+    dy = [ym - p for p in py]
+
+    def area(a, b):
+        return 0.5 * np.abs(dx[a] * dy[b] - dy[a] * dx[b])
+    S1, S2, S3 = area(1, 2), area(0, 2), area(0, 1)
+    S = S1 + S2 + S3
+    wts = [S1 / S, S2 / S, S3 / S]
+    d = np.stack([dx[k] * dx[k] + dy[k] * dy[k] for k in range(3)])
+    amin = np.argmin(d, axis=0)
+    vals = []
+    for k in range(3):
+        v = np.zeros((n,) + xm.shape, planes.dtype)
+        r, q = np.where(ok[k], rows[k], 0), np.where(ok[k], cols[k], 0)
+        v[:] = np.where(ok[k], planes[:, r, q], 0)
+        vals.append(v)
+    if interp == 1:
+        y = (wts[0] * vals[0] + wts[1] * vals[1]) + wts[2] * vals[2]
+    else:
+        y = np.choose(amin, vals) if n else np.zeros((0,) + xm.shape, planes.dtype)
+    cand = [(i_n, j_n - half1), (i_n + 1, j_n - half2), (i_n, j_n + 1 - half1),
+            (i_n + 1, j_n + 1 - half2)]
+    valid4 = sum((((r >= 0) & (r < h) & (q >= 0) & (q < w)).astype(np.int32) << k)
+                 for k, (r, q) in enumerate(cand))
+    maps = dict(i_n=i_n, j_n=j_n, flag=flag.astype(np.int32), argmin=amin, valid=valid4,
+                alpha=wts[0], beta=wts[1], gamma=wts[2], x_=xm, y_=ym)
+    return y.reshape(tuple(lead) + xm.shape), maps

@@ -324,6 +324,57 @@ def gen_conv_bwd():
     return arrs, index
 
 
+def igt_cases():
+    """(c, h, w, H, dtype) for image_geometric_transformation (hex -> hex homography)."""
+    th = np.deg2rad(30.0)
+    rot = np.array([[np.cos(th), -np.sin(th), 0.0], [np.sin(th), np.cos(th), 0.0], [0, 0, 1.0]])
+    return [
+        (1, 8, 10, np.eye(3), "f64"),
+        (3, 9, 12, np.diag([0.5, 0.5, 1.0]), "f64"),
+        (3, 12, 16, np.diag([2.0, 1.5, 1.0]), "f32"),
+        (2, 11, 13, rot, "f64"),
+        (1, 16, 16, np.array([[1.0, 0.3, 0.0], [0.2, 1.0, 0.0], [0, 0, 1.0]]), "f64"),
+        (3, 10, 14, np.array([[0.9, 0.0, 1.25], [0.0, 1.1, -2.5], [0, 0, 1.0]]), "u8"),
+        (1, 7, 9, np.array([[1.3, -0.4, 0.7], [0.5, 0.8, 0.3], [0, 0, 1.0]]), "f32"),
+    ]
+
+
+def gen_igt(rng):
+    """geometry_np.image_geometric_transformation (:6-189), 'linear', with the reference's
+    own lattice locals (its 'nearest' raises at :172, 'bilinear' returns np.empty)."""
+    arrs, index = {}, []
+    for ci, (c, h, w, Hm, dt) in enumerate(igt_cases()):
+        x = make_input(rng, (c, h, w), dt)
+        arrs[f"c{ci}_x"] = x
+        arrs[f"c{ci}_H"] = Hm
+        cap = Capture("image_geometric_transformation")
+        y = cap.run(G.image_geometric_transformation, x, Hm, "linear")
+        L = cap.locals
+        tag = f"c{ci}"
+        h1, w1 = np_(L["i_n"]).shape
+        arrs[tag + "_y"] = np.asarray(y).reshape(c, h1, w1)
+        for k in ("i_n", "j_n"):
+            arrs[tag + "_" + k] = np_(L[k]).astype(np.int32)
+        arrs[tag + "_flag"] = np_(L["up_down_flag"]).astype(np.int32)
+        arrs[tag + "_valid"] = valid_mask(L, 4)
+        arrs[tag + "_x_"] = np_(L["x_"])
+        arrs[tag + "_y_"] = np_(L["y_"])
+        for k in ("alpha", "beta", "gamma"):
+            arrs[tag + "_" + k] = np_(L[k])[..., 0]
+        for k in ("p1_x", "p1_y", "p2_x", "p2_y", "p3_x", "p3_y"):
+            arrs[tag + "_" + k] = np_(L[k])
+        entry = dict(case=ci, c=c, h=h, w=w, h1=int(h1), w1=int(w1), dtype=dt,
+                     out_dtype=str(np.asarray(y).dtype), out_shape=list(np.shape(y)))
+        try:
+            G.image_geometric_transformation(x, Hm, "nearest")
+            entry["nearest"] = "ok"
+        except Exception as e:  # the reference's tuple-unpacking of np.min (:172)
+            entry["nearest"] = type(e).__name__
+        entry["bilinear_shape"] = list(np.shape(G.image_geometric_transformation(x, Hm, "bilinear")))
+        index.append(entry)
+    return arrs, index
+
+
 def gen_taps():
     """Impulse tap tables: output (r,q) of tap t reads input flat index table[t,r,q] (-1: zero)."""
     arrs, index = {}, []
@@ -407,7 +458,8 @@ def main():
     meta = {"reference": REF, "numpy": np.__version__, "torch": torch.__version__}
     for name, fn in (("r2h", lambda: gen_r2h(rng)), ("h2r", lambda: gen_h2r(rng, gt)),
                      ("hexresize", lambda: gen_resize(rng)), ("hexconv", gen_conv),
-                     ("hexconv_bwd", gen_conv_bwd), ("taps", gen_taps)):
+                     ("hexconv_bwd", gen_conv_bwd), ("igt", lambda: gen_igt(rng)),
+                     ("taps", gen_taps)):
         arrs, index = fn()
         np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arrs)
         meta[name] = index

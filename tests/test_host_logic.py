@@ -133,3 +133,27 @@ def test_shard_range_partitions():
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             sizes = [e - s for s, e in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+def test_igt_host_plan_and_errors(golden, golden_index):
+    """image_geometric_transformation host side: the output lattice planned from the
+    transformed corners (geometry_np.py:56-87) has the reference's (h1, w1); interpolation
+    names raise like the reference (KeyError) and 'bilinear' raises instead of returning
+    np.empty (documented departure)."""
+    from HyGrid import ops
+    g = golden("igt")
+    for meta in golden_index["igt"]:
+        xs, ys, hinv = ops.homography_plan(meta["h"], meta["w"], g[f"c{meta['case']}_H"])
+        assert (xs.size, ys.size) == (meta["h1"], meta["w1"])
+        np.testing.assert_array_equal(hinv, np.linalg.inv(g[f"c{meta['case']}_H"]))
+    x = np.zeros((1, 4, 4))
+    with pytest.raises(KeyError):
+        G.image_geometric_transformation(x, np.eye(3), "cubic")
+    with pytest.raises(ValueError):
+        G.image_geometric_transformation(x, np.eye(3), "bilinear")
+    with pytest.raises(Exception):
+        G.image_geometric_transformation(np.zeros((1, 1, 1, 1, 4)), np.eye(3), "linear")
+    with pytest.raises(ValueError):
+        ops.homography_plan(4, 4, np.eye(2))
+    with pytest.raises(NotImplementedError):
+        GT.image_geometric_transformation(x, np.eye(3), "linear", device="cpu")

@@ -154,3 +154,20 @@ def test_kat_ones(golden_index):
     # S1+S2+S3 == 0.5 exactly inside the lattice => alpha+beta+gamma == 1
     s = m["alpha"] + m["beta"] + m["gamma"]
     np.testing.assert_allclose(s, 1.0, rtol=0, atol=4e-16)
+
+
+@pytest.mark.parametrize("ci", range(7))
+def test_igt_maps_and_values(golden, golden_index, ci):
+    """image_geometric_transformation (geometry_np.py:6-189): the NumPy restatement's
+    lattice (i_n, j_n, flag, validity), mapped points, weights and 'linear' output equal
+    the reference's locals bit for bit."""
+    g = golden("igt")
+    meta = golden_index["igt"][ci]
+    t = f"c{ci}"
+    y, maps = O.image_geometric_transformation(g[t + "_x"], g[t + "_H"], 1)
+    assert y.shape == (meta["c"], meta["h1"], meta["w1"])
+    for k in ("i_n", "j_n", "flag", "valid", "x_", "y_", "alpha", "beta", "gamma"):
+        np.testing.assert_array_equal(maps[k], g[t + "_" + k], err_msg=k)
+    np.testing.assert_array_equal(y, g[t + "_y"])
+    # the reference's 'nearest' raises (tuple-unpacking of np.min, :172)
+    assert meta["nearest"] == "ValueError"
