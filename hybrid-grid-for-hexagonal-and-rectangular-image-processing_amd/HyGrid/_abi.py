@@ -50,6 +50,11 @@ SIGNATURES = {
     "hg_strided_copy2d": ([_vp, _vp, _int] + [_i64] * 9 + [_vp], _int),
     "hg_hex_homography": ([_vp, _vp, _int, _int] + [_i64] * 5 + [_vp] * 3 + [_int, _vp], _int),
     "hg_hex_homography_maps": ([_i64] * 4 + [_vp] * 5 + [_vp], _int),
+    "hg_hex_pool2d": ([_vp, _vp, _int, _int] + [_i64] * 3 + [_int, _int, _dbl, _i64, _i64, _dbl]
+                      + [_int] * 4 + [_i64, _i64, _vp], _int),
+    "hg_hex_pool2d_backward": ([_vp, _vp, _vp, _int, _int, _int] + [_i64] * 3
+                               + [_int, _int, _dbl, _i64, _i64, _dbl] + [_int] * 4
+                               + [_i64, _i64, _vp], _int),
     "hg_pipeline_r2h_conv_h2r": ([_vp, _vp, _vp, _vp, _int, _int] + [_i64] * 9 +
                                  [_int, _int, _int, _dbl, _vp], _int),
 }

@@ -192,6 +192,113 @@ def homography_maps(h, w, H, device=None):
     return out
 
 
+POOL_METHODS = {"max": 0, "min": 1, "average": 2}
+_POOL_PAD_MODES = _abi.PAD_MODES
+
+
+def pool_plan(h, w, kh, kw, sh, sw, padding=0, ceil_mode=False, count_include_pad=True):
+    """HexPool2d's window geometry (HexFrames.py:286-319): the padded frame, the ceil-mode
+    extension (F.pad(input, (0, ph, 0, pw)) — ph columns on the right, pw rows at the
+    bottom, as the reference passes them, :295-300) and the output size.  Returns
+    dict(hn, wn, ext_h, ext_w, ext_value).  Raises IndexError where the reference's
+    gather would index outside the frame."""
+    H0, W0 = h + 2 * padding, w + 2 * padding
+    ext_h = ext_w = 0
+    ext_value = 0.0
+    if ceil_mode:
+        hn0 = H0 // sh
+        wn0 = (W0 - sw // 2 - sw) // sw + 1
+        ph = (kh - H0 + hn0 * sh) % kh
+        pw = (kw - W0 + (wn0 * sw + sw // 2)) % kw
+        ext_w, ext_h = ph, pw
+        ext_value = 0.0 if count_include_pad else float("nan")
+    H, W = H0 + ext_h, W0 + ext_w
+    hn = (H - kh) // sh + 1
+    wn = (W - sw // 2) // sw
+    if hn < 0 or wn < 0:
+        raise RuntimeError(f"hex pooling: window {kh}x{kw} / stride {sh}x{sw} does not fit "
+                           f"a {H}x{W} frame")
+    if hn > 0 and wn > 0:
+        shift = sw // 2 if hn >= 2 else 0
+        if (hn - 1) * sh + kh > H or (wn - 1) * sw + shift + kw > W:
+            raise IndexError(f"hex pooling: windows ({kh}x{kw}, stride {sh}x{sw}) reach "
+                             f"outside the {H}x{W} frame (the reference's gather raises)")
+    return dict(hn=hn, wn=wn, ext_h=ext_h, ext_w=ext_w, ext_value=ext_value)
+
+
+def _pool_args(x, method, kh, kw, sh, sw, hn, wn, pad, pad_mode, pad_value, ext_h, ext_w,
+               ext_value):
+    h, w = int(x.shape[-2]), int(x.shape[-1])
+    return (POOL_METHODS[method], h, w, int(pad), _POOL_PAD_MODES[pad_mode], float(pad_value),
+            int(ext_h), int(ext_w), float(ext_value), int(kh), int(kw), int(sh), int(sw),
+            int(hn), int(wn))
+
+
+def _pool_raw(x, args):
+    _abi.require_device(x)
+    if x.dtype not in _FLOATS:
+        raise TypeError(f"hex pooling needs a floating-point raster, got {x.dtype} (the "
+                        f"reference's NaN masking, HexFrames.py:461-479)")
+    x, lead, planes = _planes(x.detach())
+    m, h, w, pad, mode, pv, eh, ew, ev, kh, kw, sh, sw, hn, wn = args
+    y = torch.empty(lead + (hn, wn), dtype=x.dtype, device=x.device)
+    st = _abi.lib().hg_hex_pool2d(_abi.ptr(x), _abi.ptr(y), _abi.dtype_code(x.dtype), m, planes,
+                                  h, w, pad, mode, pv, eh, ew, ev, kh, kw, sh, sw, hn, wn,
+                                  _abi.stream_of(x))
+    _abi.check(st, "hg_hex_pool2d")
+    return y
+
+
+class _HexPoolFn(torch.autograd.Function):
+    """Autograd of hex pooling: hg_hex_pool2d_backward (gy to the selected element of a
+    max / min window, gy / count to the non-NaN elements of an average window, folded
+    back through the padding) — the reference's autograd of HexFrames.py:286-343."""
+
+    @staticmethod
+    def forward(ctx, x, args):
+        ctx.save_for_backward(x)
+        ctx.args = args
+        return _pool_raw(x, args)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        m, h, w, pad, mode, pv, eh, ew, ev, kh, kw, sh, sw, hn, wn = ctx.args
+        acc = torch.float64 if x.dtype == torch.float64 else torch.float32
+        xc, lead, planes = _planes(x.detach())
+        g = gy.contiguous().to(acc)
+        dx = torch.empty(tuple(x.shape), dtype=acc, device=x.device)
+        st = _abi.lib().hg_hex_pool2d_backward(
+            _abi.ptr(xc), _abi.ptr(g), _abi.ptr(dx), _abi.dtype_code(x.dtype),
+            _abi.dtype_code(acc), m, planes, h, w, pad, mode, pv, eh, ew, ev, kh, kw, sh, sw,
+            hn, wn, _abi.stream_of(xc))
+        _abi.check(st, "hg_hex_pool2d_backward")
+        return dx.to(x.dtype), None
+
+
+def hex_pool2d(x, method, kh, kw, sh, sw, hn, wn, pad=0, pad_mode="constant", pad_value=0.0,
+               ext_h=0, ext_w=0, ext_value=0.0):
+    """Hex pooling of (..., h, w) -> (..., hn, wn) by hg_hex_pool2d (geometry: pool_plan).
+    Differentiable in x."""
+    if pad_mode not in _POOL_PAD_MODES:
+        raise NotImplementedError(f"padding mode {pad_mode!r}")
+    if _POOL_PAD_MODES[pad_mode] != 0 and pad_value not in (0, None):
+        raise RuntimeError(f'Padding mode "{pad_mode}" doesn\'t take in value argument')
+    args = _pool_args(x, method, kh, kw, sh, sw, hn, wn, pad, pad_mode,
+                      0.0 if pad_value is None else pad_value, ext_h, ext_w, ext_value)
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _HexPoolFn.apply(x, args)
+    return _pool_raw(x, args)
+
+
+def reduce_last(x, method):
+    """The reference's max_pooling / min_pooling / average_pooling (HexFrames.py:461-479):
+    NaN-aware reduction over the last dim, as a 1 x n window of hg_hex_pool2d."""
+    n = int(x.shape[-1])
+    y = hex_pool2d(x.unsqueeze(-2), method, 1, n, 1, max(n, 1), 1, 1)
+    return y[..., 0, 0]
+
+
 def hexconv2d_out_shape(h, w, radius, stride=1, padding=0, dilation=1):
     ho, wo = ctypes.c_int64(), ctypes.c_int64()
     st = _abi.lib().hg_hexconv2d_out_shape(h, w, radius, stride, padding, dilation,

@@ -158,6 +158,24 @@ int hg_strided_copy2d(const void* src, void* dst, int elem_size, int64_t planes,
 int hg_hex_homography(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t planes,
                       int64_t h, int64_t w, int64_t h1, int64_t w1, const double* xs,
                       const double* ys, const double* hinv, int interp, void* stream);
+/* Hex pooling: replaces HexPool2d / HexAdaptivePool2d / HexGlobalPool2d
+ * (HexFrames.py:255-410) with the NaN-aware reductions max_pooling / min_pooling /
+ * average_pooling (:461-479); method 0 max, 1 min, 2 average.  x: (planes, h, w) of
+ * dtype F16/BF16/F32/F64, y: (planes, hn, wn) of the same dtype.  Window (i, j) covers
+ * rows i*sh + [0, kh) and cols ((i % 2) * sw) / 2 + j*sw + [0, kw) (:314-319) of the
+ * frame pad(x, pad, pad_mode, pad_value) extended by ext_h rows / ext_w cols of
+ * ext_value (ceil mode, :295-300).  Windows outside the frame -> HG_ESHAPE (the
+ * reference raises IndexError).  Backward: dx (planes, h, w) in grad_dtype F32/F64
+ * (overwritten) from gy (planes, hn, wn) in grad_dtype, the reference's autograd. */
+int hg_hex_pool2d(const void* x, void* y, int dtype, int method, int64_t planes, int64_t h,
+                  int64_t w, int pad, int pad_mode, double pad_value, int64_t ext_h,
+                  int64_t ext_w, double ext_value, int kh, int kw, int sh, int sw, int64_t hn,
+                  int64_t wn, void* stream);
+int hg_hex_pool2d_backward(const void* x, const void* gy, void* dx, int dtype, int grad_dtype,
+                           int method, int64_t planes, int64_t h, int64_t w, int pad,
+                           int pad_mode, double pad_value, int64_t ext_h, int64_t ext_w,
+                           double ext_value, int kh, int kw, int sh, int sw, int64_t hn,
+                           int64_t wn, void* stream);
 int hg_hex_homography_maps(int64_t h, int64_t w, int64_t h1, int64_t w1, const double* xs,
                            const double* ys, const double* hinv, int32_t* imaps, double* fmaps,
                            void* stream);

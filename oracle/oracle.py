@@ -14,6 +14,8 @@ Each function mirrors one reference entry point (paths under /root/reference):
   hexconv2d_backward  the adjoint of hexconv2d (reference: torch autograd of :96-169)
   image_geometric_transformation  HyGrid/geometry_np.py:6-189 (NumPy restatement;
                 nearest per HyGrid/geometry_torch.py:165-173)
+  hex_pool2d    HyGrid/HexFrames.py:286-343 windows, :461-479 reductions, and their
+                autograd (hex_pool2d_backward)
 Inputs are (planes, h, w) arrays of any real dtype; outputs are float64.
 """
 import ctypes
@@ -257,3 +259,93 @@ def image_geometric_transformation(x, H, interp=1):
     maps = dict(i_n=i_n, j_n=j_n, flag=flag.astype(np.int32), argmin=amin, valid=valid4,
                 alpha=wts[0], beta=wts[1], gamma=wts[2], x_=xm, y_=ym)
     return y.reshape(tuple(lead) + xm.shape), maps
+
+
+_PAD_NP = {"constant": "constant", "zeros": "constant", "reflect": "reflect",
+           "replicate": "edge", "circular": "wrap"}
+
+
+def _pool_frame(x, pad, mode, value, ext_h, ext_w, ext_value):
+    """The reference's padded (+ ceil-mode extended) input (:289, :300), with the index
+    of each frame element in x (-1 outside x) for the backward fold."""
+    n, h, w = x.shape
+    idx = np.arange(h * w, dtype=np.int64).reshape(h, w)
+    if pad:
+        m = _PAD_NP[mode]
+        if m == "constant":
+            f = np.pad(x, ((0, 0), (pad, pad), (pad, pad)), constant_values=value)
+            idx = np.pad(idx, pad, constant_values=-1)
+        else:
+            f = np.pad(x, ((0, 0), (pad, pad), (pad, pad)), mode=m)
+            idx = np.pad(idx, pad, mode=m)
+    else:
+        f = x
+    if ext_h or ext_w:
+        f = np.pad(f, ((0, 0), (0, ext_h), (0, ext_w)), constant_values=ext_value)
+        idx = np.pad(idx, ((0, ext_h), (0, ext_w)), constant_values=-1)
+    return f, idx
+
+
+def _pool_windows(hn, wn, kh, kw, sh, sw):
+    """Frame (row, col) of every window element, (hn, wn, kh*kw) each (:307-325)."""
+    i = np.arange(hn)[:, None, None]
+    j = np.arange(wn)[None, :, None]
+    k = np.arange(kh * kw)[None, None, :]
+    rows = i * sh + k // kw
+    cols = (i % 2) * sw // 2 + j * sw + k % kw
+    return np.broadcast_to(rows, (hn, wn, kh * kw)), np.broadcast_to(cols, (hn, wn, kh * kw))
+
+
+def hex_pool2d(x, method, kh, kw, sh, sw, hn, wn, pad=0, mode="constant", value=0.0,
+               ext_h=0, ext_w=0, ext_value=0.0):
+    """NumPy restatement of hex pooling on (..., h, w) float64 input -> (..., hn, wn):
+    window gather (:307-325) then max_pooling / min_pooling / average_pooling
+    (:461-479: NaN -> -inf / +inf, first extreme; mean of the non-NaN values)."""
+    planes, lead = _as_planes(x)
+    f, _ = _pool_frame(planes, pad, mode, value, ext_h, ext_w, ext_value)
+    r, c = _pool_windows(hn, wn, kh, kw, sh, sw)
+    g = f[:, r, c]                                         # (n, hn, wn, K)
+    nan = np.isnan(g)
+    if method == "max":
+        y = np.where(nan, -np.inf, g).max(axis=-1) if g.shape[-1] else None
+    elif method == "min":
+        y = np.where(nan, np.inf, g).min(axis=-1) if g.shape[-1] else None
+    else:
+        cnt = (~nan).sum(axis=-1)
+        ssum = np.where(nan, 0.0, g).sum(axis=-1)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            y = ssum / cnt
+        y[cnt == 0] = np.nan
+    return y.reshape(tuple(lead) + (hn, wn))
+
+
+def hex_pool2d_backward(x, gy, method, kh, kw, sh, sw, hn, wn, pad=0, mode="constant",
+                        value=0.0, ext_h=0, ext_w=0, ext_value=0.0):
+    """d x of hex_pool2d (the reference's autograd): max / min give gy to the first
+    extreme unless it is NaN or padding; average gives gy / count to each non-NaN
+    element; padded positions fold back onto x (reflect / replicate / circular)."""
+    planes, lead = _as_planes(x)
+    gyp = np.asarray(gy, np.float64).reshape(-1, hn, wn)
+    n = planes.shape[0]
+    f, idx = _pool_frame(planes, pad, mode, value, ext_h, ext_w, ext_value)
+    r, c = _pool_windows(hn, wn, kh, kw, sh, sw)
+    g = f[:, r, c]
+    src = idx[r, c]                                        # (hn, wn, K)
+    nan = np.isnan(g)
+    dx = np.zeros(planes.shape[0:1] + (planes.shape[1] * planes.shape[2],))
+    if method in ("max", "min"):
+        u = np.where(nan, -np.inf if method == "max" else np.inf, g)
+        sel = u.argmax(axis=-1) if method == "max" else u.argmin(axis=-1)
+        s = np.take_along_axis(src[None].repeat(n, 0), sel[..., None], -1)[..., 0]
+        ok = (s >= 0) & ~np.take_along_axis(nan, sel[..., None], -1)[..., 0]
+        for p in range(n):
+            np.add.at(dx[p], s[p][ok[p]], gyp[p][ok[p]])
+    else:
+        cnt = (~nan).sum(axis=-1)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            gs = gyp / cnt
+        contrib = np.where(nan | (src[None] < 0), 0.0, gs[..., None])
+        for p in range(n):
+            m = (src >= 0) & ~nan[p]
+            np.add.at(dx[p], src[m], contrib[p][m])
+    return dx.reshape(np.shape(x))

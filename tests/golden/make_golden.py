@@ -21,6 +21,8 @@ Reference call sites exercised (paths relative to /root/reference):
                          numpy's linspace so the lattice is the geometry_np one.
   hexresize              HyGrid/geometry_np.py:520-681
   HexConv2d              HyGrid/HexFrames.py:22-185 (+ heximage_to_type1 :417-445)
+  image_geometric_transformation  HyGrid/geometry_np.py:6-189
+  HexPool2d / HexAdaptivePool2d / HexGlobalPool2d  HyGrid/HexFrames.py:255-410, :461-479
 
 Usage:  python tests/golden/make_golden.py   (writes next to this file)
 """
@@ -375,6 +377,107 @@ def gen_igt(rng):
     return arrs, index
 
 
+def pool_cases():
+    """HexPool2d configurations (HexFrames.py:255-343).  stride is always given: the
+    reference's stride=None path crashes (:270-276)."""
+    return [
+        dict(method="max", k=2, s=2, pad=0, h=8, w=11),
+        dict(method="min", k=2, s=2, pad=0, h=9, w=12),
+        dict(method="average", k=2, s=2, pad=0, h=8, w=12),
+        dict(method="max", k=3, s=2, pad=1, h=10, w=13),
+        dict(method="average", k=3, s=3, pad=1, h=12, w=16, mode="reflect"),
+        dict(method="max", k=[2, 3], s=[2, 3], pad=0, h=9, w=14),
+        dict(method="average", k=2, s=2, pad=0, h=9, w=13, ceil=True),
+        dict(method="average", k=2, s=2, pad=0, h=9, w=13, ceil=True, cip=False),
+        dict(method="max", k=3, s=3, pad=0, h=11, w=16, ceil=True, cip=False),
+        dict(method="average", k=2, s=1, pad=1, h=7, w=9, mode="replicate"),
+        dict(method="min", k=2, s=2, pad=2, h=6, w=8, mode="constant", value=0.5),
+        dict(method="max", k=2, s=2, pad=0, h=8, w=10, allnan=True),
+        dict(method="average", k=2, s=2, pad=0, h=8, w=10, allnan=True),
+        dict(method="max", k=4, s=2, pad=0, h=9, w=12),
+        dict(method="average", k=2, s=2, pad=1, h=7, w=9, mode="circular"),
+        dict(method="max", k=3, s=2, pad=1, h=10, w=12),
+        dict(method="average", k=3, s=2, pad=0, h=9, w=10, ceil=True, cip=False),
+        dict(method="min", k=[3, 2], s=[2, 3], pad=1, h=11, w=15, ceil=True),
+        dict(method="max", k=2, s=3, pad=0, h=10, w=14),
+    ]
+
+
+def _nan_input(shape, seed, allnan=False):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(shape, generator=g, dtype=torch.float64)
+    m = torch.rand(shape, generator=g) < 0.15
+    x[m] = float("nan")
+    if allnan:
+        x[..., 0:2, 0:4] = float("nan")      # whole windows of NaN
+    return x
+
+
+def gen_pool():
+    """HexPool2d / HexAdaptivePool2d / HexGlobalPool2d outputs and input gradients from the
+    reference's own forward and autograd (NaN-aware max/min/average, :461-479).  The
+    adaptive / global modules cannot be constructed in the reference (their method dict
+    names the undefined centroid_pooling, :354-358, :401-405); their forward (:359-396,
+    :406-410) is run on instances built with nn.Module.__init__ and the method set."""
+    arrs, index = {}, []
+    ci = 0
+    for p in pool_cases():
+        x = _nan_input((2, 3, p["h"], p["w"]), 500 + ci, p.get("allnan", False))
+        entry = dict(kind="pool", case=ci, **p)
+        try:
+            m = HF.HexPool2d(p["method"], kernel_size=p["k"], stride=p["s"], padding=p["pad"],
+                             padding_mode=p.get("mode", "constant"),
+                             padding_value=p.get("value", 0), ceil_mode=p.get("ceil", False),
+                             count_include_pad=p.get("cip", True))
+            xr = x.clone().requires_grad_(True)
+            y = m(xr)
+            gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(900 + ci),
+                             dtype=torch.float64)
+            y.backward(gy)
+            arrs[f"p{ci}_x"] = x.numpy()
+            arrs[f"p{ci}_y"] = y.detach().numpy()
+            arrs[f"p{ci}_gy"] = gy.numpy()
+            arrs[f"p{ci}_dx"] = xr.grad.numpy()
+            entry["out_shape"] = list(y.shape)
+        except Exception as e:
+            entry["error"] = type(e).__name__
+        index.append(entry)
+        ci += 1
+    for kind, cls, args in (("adaptive", "HexAdaptivePool2d", [(2, 9, 12), (3, 12, 20),
+                                                                  (4, 8, 9), (1, 6, 7)]),
+                            ("global", "HexGlobalPool2d", [(1, 5, 7), (1, 16, 20)])):
+        for a in args:
+            for method in ("max", "min", "average"):
+                entry = dict(kind=kind, case=ci, method=method, outsize=a[0], h=a[1], w=a[2])
+                try:
+                    getattr(HF, cls)(a[0], method) if kind == "adaptive" else getattr(HF, cls)(method)
+                    entry["construct"] = "ok"
+                except Exception as e:
+                    entry["construct"] = type(e).__name__
+                m = getattr(HF, cls).__new__(getattr(HF, cls))
+                torch.nn.Module.__init__(m)
+                m.hn, m.wn = a[0], a[0]
+                m.method = {"max": HF.max_pooling, "min": HF.min_pooling,
+                            "average": HF.average_pooling}[method]
+                x = _nan_input((2, 3, a[1], a[2]), 700 + ci)
+                xr = x.clone().requires_grad_(True)
+                try:
+                    y = m(xr)
+                    gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(ci),
+                                     dtype=torch.float64)
+                    y.backward(gy)
+                    arrs[f"p{ci}_x"] = x.numpy()
+                    arrs[f"p{ci}_y"] = y.detach().numpy()
+                    arrs[f"p{ci}_gy"] = gy.numpy()
+                    arrs[f"p{ci}_dx"] = xr.grad.numpy()
+                    entry["out_shape"] = list(y.shape)
+                except Exception as e:
+                    entry["error"] = type(e).__name__
+                index.append(entry)
+                ci += 1
+    return arrs, index
+
+
 def gen_taps():
     """Impulse tap tables: output (r,q) of tap t reads input flat index table[t,r,q] (-1: zero)."""
     arrs, index = {}, []
@@ -459,7 +562,7 @@ def main():
     for name, fn in (("r2h", lambda: gen_r2h(rng)), ("h2r", lambda: gen_h2r(rng, gt)),
                      ("hexresize", lambda: gen_resize(rng)), ("hexconv", gen_conv),
                      ("hexconv_bwd", gen_conv_bwd), ("igt", lambda: gen_igt(rng)),
-                     ("taps", gen_taps)):
+                     ("pool", gen_pool), ("taps", gen_taps)):
         arrs, index = fn()
         np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arrs)
         meta[name] = index

@@ -157,3 +157,35 @@ def test_igt_host_plan_and_errors(golden, golden_index):
         ops.homography_plan(4, 4, np.eye(2))
     with pytest.raises(NotImplementedError):
         GT.image_geometric_transformation(x, np.eye(3), "linear", device="cpu")
+
+
+def test_pool_host_surface(golden_index):
+    """Hex pooling host logic: window planning raises where the reference's gather does,
+    constructor / repr parity, and the documented departures (stride=None, constructible
+    adaptive / global modules, 'centroid' -> NotImplementedError)."""
+    from HyGrid import ops
+    from pool_cases import pool_args
+    for m in golden_index["pool"]:
+        if "error" in m:
+            assert m["error"] == "IndexError"
+            with pytest.raises(IndexError):
+                pool_args(m)
+        else:
+            a = pool_args(m)
+            assert list(m["out_shape"][-2:]) == [a[5], a[6]] or m["kind"] == "global"
+        if m["kind"] != "pool":
+            assert m["construct"] == "NameError"     # the reference's centroid_pooling
+    p = HexFrames.HexPool2d("max", 2, 2)
+    assert repr(p) == "HexPool2d(kernel_size=[2, 2], stride=[2, 2], padding=0)"
+    assert HexFrames.HexPool2d("average", 3).stride == [3, 3]          # stride=None
+    with pytest.raises(KeyError):
+        HexFrames.HexPool2d("median", 2, 2)
+    with pytest.raises(NotImplementedError):
+        HexFrames.HexAdaptivePool2d(2, "centroid")
+    with pytest.raises(NotImplementedError):
+        HexFrames.HexGlobalPool2d("centroid")
+    assert HexFrames.HexAdaptivePool2d([2, 3], "max").wn == 3
+    with pytest.raises(Exception):
+        HexFrames.HexAdaptivePool2d(2.5, "max")
+    with pytest.raises(RuntimeError):
+        ops.hex_pool2d(torch.zeros(1, 1, 4, 4), "max", 2, 2, 2, 2, 2, 1, 1, "reflect", 1.0)

@@ -171,3 +171,27 @@ def test_igt_maps_and_values(golden, golden_index, ci):
     np.testing.assert_array_equal(y, g[t + "_y"])
     # the reference's 'nearest' raises (tuple-unpacking of np.min, :172)
     assert meta["nearest"] == "ValueError"
+
+
+def test_pool_oracle_vs_reference(golden, golden_index):
+    """Hex pooling (HexFrames.py:255-410, :461-479): the NumPy restatement's outputs and
+    input gradients against the reference's forward and autograd.  max / min exact;
+    average within 4 ulp (torch's vectorised window sum order differs from NumPy's)."""
+    from pool_cases import pool_args
+    g = golden("pool")
+    n_ok = 0
+    for m in golden_index["pool"]:
+        if "error" in m:
+            continue
+        t = f"p{m['case']}"
+        args = pool_args(m)
+        y = O.hex_pool2d(g[t + "_x"], *args)
+        yr = g[t + "_y"].reshape(y.shape)
+        if m["method"] == "average":
+            np.testing.assert_allclose(y, yr, rtol=1e-15, atol=5e-16)
+        else:
+            np.testing.assert_array_equal(y, yr)
+        dx = O.hex_pool2d_backward(g[t + "_x"], g[t + "_gy"], *args)
+        np.testing.assert_allclose(dx, g[t + "_dx"], rtol=1e-15, atol=1e-16)
+        n_ok += 1
+    assert n_ok >= 30
