@@ -7,13 +7,23 @@ behaviour.  If mmcv is importable, HexConv2d is registered in its CONV_LAYERS
 registry exactly like the reference (:16) and mmcv's builders are used; if not
 (it is absent from this image), a small local registry with the same semantics
 covers the layer types the reference's configs use.
+
+Epilogue fusion: when the block is conv -> BatchNorm (running statistics) -> an
+elementwise activation, or conv -> activation, `forward` runs ONE gfx950 launch
+(hg_hexconv2d_epilogue): the BatchNorm is folded into a per-channel scale / shift and
+applied with the bias and the activation in the conv's store, so neither the norm nor
+the activation re-reads the conv output.  The unfused torch sequence is kept for
+training-mode / non-batch norms, trainable norm parameters under autograd, spectral
+norm, other orders and activations.  `fused=False` on the module forces it.
 """
 import warnings
 from typing import Dict, Optional, Tuple, Union
 
+import torch
 import torch.nn as nn
 
 from . import HexFrames as hnn
+from . import _abi, ops
 
 try:  # the reference hard-requires mmcv (:7-12); here it is optional
     from mmcv.cnn.bricks.activation import build_activation_layer as _mm_act
@@ -159,6 +169,56 @@ def _constant_init(module, val, bias=0):
 
 _NORM_BATCH_INSTANCE = (nn.modules.batchnorm._BatchNorm, nn.modules.instancenorm._InstanceNorm)
 
+_FUSED_ACTS = {nn.ReLU: _abi.HG_ACT_RELU, nn.LeakyReLU: _abi.HG_ACT_LEAKY_RELU,
+               nn.ReLU6: _abi.HG_ACT_RELU6, nn.Sigmoid: _abi.HG_ACT_SIGMOID,
+               nn.Tanh: _abi.HG_ACT_TANH}
+
+
+def _act_grad(y, act, slope):
+    """d act / d pre-activation, from the activation's output (torch's own rules:
+    threshold_backward on the result for ReLU, hardtanh bounds for ReLU6)."""
+    if act == _abi.HG_ACT_RELU:
+        return (y > 0).to(y.dtype)
+    if act == _abi.HG_ACT_LEAKY_RELU:
+        return torch.where(y > 0, torch.ones_like(y), torch.full_like(y, slope))
+    if act == _abi.HG_ACT_RELU6:
+        return ((y > 0) & (y < 6)).to(y.dtype)
+    if act == _abi.HG_ACT_SIGMOID:
+        return y * (1 - y)
+    if act == _abi.HG_ACT_TANH:
+        return 1 - y * y
+    return None
+
+
+class _HexConvEpilogueFn(torch.autograd.Function):
+    """conv + bias -> x scale + shift -> act in one launch; backward through the
+    activation (from the saved output) and the fixed affine into hexconv2d_backward."""
+
+    @staticmethod
+    def forward(ctx, x, kernel, bias, cfg, scale, shift, act, slope):
+        y = ops.hexconv2d(x, kernel, bias, cfg["off"], cfg["r"], cfg["stride"], cfg["pad"],
+                          cfg["dilation"], cfg["groups"], cfg["padding_mode"],
+                          cfg["padding_value"], cfg["out_dtype"],
+                          epilogue=(scale, shift, act, slope))
+        ctx.save_for_backward(x, kernel, bias, y, scale)
+        ctx.meta = (cfg, act, slope)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, kernel, bias, y, scale = ctx.saved_tensors
+        cfg, act, slope = ctx.meta
+        g = gy
+        d = _act_grad(y, act, slope)
+        if d is not None:
+            g = g * d
+        if scale is not None:
+            g = g * scale.to(g.dtype).view(1, -1, 1, 1)
+        need_x, need_k, need_b = ctx.needs_input_grad[:3]
+        gx, gk, gb = ops.hexconv2d_backward(g, x, kernel, bias, cfg, need_x, need_k, need_b)
+        return gx, gk, gb, None, None, None, None, None
+
+
 
 class HexConvModule(nn.Module):
     """conv/norm/act block around HexConv2d (HexModules.py:97-288)."""
@@ -255,7 +315,50 @@ class HexConvModule(nn.Module):
         if self.with_norm:
             _constant_init(self.norm, 1, bias=0)
 
+    fused = True
+
+    def _epilogue_plan(self, x, activate, norm):
+        """(scale, shift, act, slope) when conv -> norm -> act folds into the conv's
+        epilogue, else None."""
+        if not self.fused or self.order != ('conv', 'norm', 'act') or self.with_spectral_norm:
+            return None
+        if type(self.conv) is not hnn.HexConv2d or not x.is_cuda:
+            return None
+        act, slope = _abi.HG_ACT_NONE, 0.0
+        if activate and self.with_activation:
+            act = _FUSED_ACTS.get(type(self.activate))
+            if act is None:
+                return None
+            if act == _abi.HG_ACT_LEAKY_RELU:
+                slope = float(self.activate.negative_slope)
+                if slope < 0:
+                    return None
+        scale = shift = None
+        if norm and self.with_norm:
+            bn = self.norm
+            if not isinstance(bn, nn.modules.batchnorm._BatchNorm) or bn.training or \
+                    bn.running_mean is None:
+                return None
+            if torch.is_grad_enabled() and any(p.requires_grad for p in bn.parameters()):
+                return None
+            inv = torch.rsqrt(bn.running_var.double() + bn.eps)
+            w = bn.weight.detach().double() if bn.weight is not None else 1.0
+            b = bn.bias.detach().double() if bn.bias is not None else 0.0
+            scale = (w * inv).float()
+            shift = (b - bn.running_mean.double() * w * inv).float()
+        if act == _abi.HG_ACT_NONE and scale is None:
+            return None
+        return scale, shift, act, slope
+
     def forward(self, x, activate: bool = True, norm: bool = True):
+        plan = self._epilogue_plan(x, activate, norm)
+        if plan is not None:
+            if self.with_explicit_padding:
+                x = self.padding_layer(x)
+            while x.dim() < 4:
+                x = x.unsqueeze(0)
+            return _HexConvEpilogueFn.apply(x, self.conv.kernel, self.conv.bias,
+                                            self.conv._cfg(), *plan)
         for layer in self.order:
             if layer == 'conv':
                 if self.with_explicit_padding:

@@ -20,6 +20,7 @@ HG_U8, HG_I8, HG_U16, HG_I16, HG_I32, HG_I64, HG_F16, HG_BF16, HG_F32, HG_F64 = 
 HG_NEAREST, HG_LINEAR = 0, 1
 HG_OP_RECT_TO_HEX, HG_OP_HEX_TO_RECT, HG_OP_HEXRESIZE = 0, 1, 2
 PAD_MODES = {"constant": 0, "zeros": 0, "reflect": 1, "replicate": 2, "circular": 3}
+HG_ACT_NONE, HG_ACT_RELU, HG_ACT_LEAKY_RELU, HG_ACT_RELU6, HG_ACT_SIGMOID, HG_ACT_TANH = range(6)
 
 TORCH_DTYPE = {
     torch.uint8: HG_U8, torch.int8: HG_I8, torch.int16: HG_I16, torch.int32: HG_I32,
@@ -44,6 +45,9 @@ SIGNATURES = {
                                 ctypes.POINTER(_i64), ctypes.POINTER(_i64)], _int),
     "hg_hexconv2d": ([_vp, _vp, _vp, _vp, _int, _int, _int, _i64, _i64, _i64, _i64, _i64,
                       _int, _int, _int, _int, _int, _int, _int, _dbl, _vp], _int),
+    "hg_hexconv2d_epilogue": ([_vp, _vp, _vp, _vp, _int, _int, _int, _i64, _i64, _i64, _i64,
+                               _i64, _int, _int, _int, _int, _int, _int, _int, _dbl, _vp, _vp,
+                               _int, _dbl, _vp], _int),
     "hg_hexconv2d_backward": ([_vp] * 6 + [_int, _int] + [_i64] * 5 + [_int] * 7 + [_dbl, _vp],
                               _int),
     "hg_hex_to_type1": ([_vp, _vp, _int] + [_i64] * 3 + [_int, _int, _vp], _int),

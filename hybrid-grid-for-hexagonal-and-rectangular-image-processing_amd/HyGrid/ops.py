@@ -308,11 +308,14 @@ def hexconv2d_out_shape(h, w, radius, stride=1, padding=0, dilation=1):
 
 
 def hexconv2d(x, kernel, bias, even_odd_offset, radius, stride=1, padding=0, dilation=1,
-              groups=1, padding_mode="constant", padding_value=0.0, out_dtype=None):
+              groups=1, padding_mode="constant", padding_value=0.0, out_dtype=None,
+              epilogue=None):
     """HexConv2d forward (HexFrames.py:96-169) on (B, C, H, W) -> (B, O, Ho, Wo).
 
     kernel: (O, C/groups, 1, K) or (O, C/groups, K) float32/float64 — the
     accumulation dtype, as the reference's `input.to(self.kernel.dtype)` (:107).
+    epilogue: None or (scale, shift, act, slope) — per-channel affine (tensors (O,) or
+    None) and hg_act activation fused into the store (hg_hexconv2d_epilogue).
     """
     _abi.require_device(x)
     while x.dim() < 4:
@@ -336,12 +339,26 @@ def hexconv2d(x, kernel, bias, even_odd_offset, radius, stride=1, padding=0, dil
     pm = _abi.PAD_MODES.get(padding_mode)
     if pm is None:
         raise ValueError(f"unsupported padding_mode {padding_mode!r}")
-    st = _abi.lib().hg_hexconv2d(
+    if epilogue is None:
+        st = _abi.lib().hg_hexconv2d(
+            _abi.ptr(x), _abi.ptr(k), _abi.ptr(b), _abi.ptr(y), _abi.dtype_code(x.dtype),
+            _abi.dtype_code(k.dtype), _abi.dtype_code(out_dtype), B, C, O, h, w, radius, stride,
+            padding, dilation, groups, int(even_odd_offset), pm, float(padding_value),
+            _abi.stream_of(x))
+        _abi.check(st, "hg_hexconv2d")
+        return y
+    scale, shift, act, slope = epilogue
+    sc = None if scale is None else scale.detach().to(k.dtype).contiguous()
+    sf = None if shift is None else shift.detach().to(k.dtype).contiguous()
+    for t in (sc, sf):
+        if t is not None and t.numel() != O:
+            raise ValueError(f"epilogue scale/shift must have {O} elements")
+    st = _abi.lib().hg_hexconv2d_epilogue(
         _abi.ptr(x), _abi.ptr(k), _abi.ptr(b), _abi.ptr(y), _abi.dtype_code(x.dtype),
         _abi.dtype_code(k.dtype), _abi.dtype_code(out_dtype), B, C, O, h, w, radius, stride,
         padding, dilation, groups, int(even_odd_offset), pm, float(padding_value),
-        _abi.stream_of(x))
-    _abi.check(st, "hg_hexconv2d")
+        _abi.ptr(sc), _abi.ptr(sf), int(act), float(slope), _abi.stream_of(x))
+    _abi.check(st, "hg_hexconv2d_epilogue")
     return y
 
 

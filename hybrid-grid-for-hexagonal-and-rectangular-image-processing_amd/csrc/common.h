@@ -66,6 +66,29 @@ __device__ __forceinline__ void xcd_swizzle2(unsigned* bx, unsigned* by) {
     *by = s / gridDim.x;
 }
 
+// Fused conv epilogue (hg_hexconv2d_epilogue): v -> act(scale[o] * v + shift[o]).
+struct Epilogue {
+    const void* scale;   // (O,) accumulator type, or null (1)
+    const void* shift;   // (O,) accumulator type, or null (0)
+    int act;             // hg_act
+    double slope;        // LeakyReLU negative slope
+    int on;              // any of the above present
+};
+
+template <typename A>
+__device__ __forceinline__ A epi_apply(A v, int o, const Epilogue& e) {
+    if (e.scale) v = v * static_cast<const A*>(e.scale)[o];
+    if (e.shift) v = v + static_cast<const A*>(e.shift)[o];
+    switch (e.act) {
+    case HG_ACT_RELU: return v > (A)0 ? v : (A)0;
+    case HG_ACT_LEAKY_RELU: return v > (A)0 ? v : v * (A)e.slope;
+    case HG_ACT_RELU6: return v > (A)0 ? (v < (A)6 ? v : (A)6) : (A)0;
+    case HG_ACT_SIGMOID: return (A)1 / ((A)1 + exp(-v));
+    case HG_ACT_TANH: return tanh(v);
+    default: return v;
+    }
+}
+
 }  // namespace hg
 
 // Instantiate `FN<Tin, Tout>(args...)` for every supported (in, out) dtype pair.

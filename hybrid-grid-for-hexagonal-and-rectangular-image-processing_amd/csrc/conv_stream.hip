@@ -25,6 +25,7 @@ struct ConvStreamGeom {
     int h, w, ho, wo, p;
     float padv;
     int HL, nown, nwin, nband, RB;
+    Epilogue epi;
 };
 
 typedef float float2v_cs __attribute__((ext_vector_type(2)));
@@ -207,7 +208,9 @@ __global__ __launch_bounds__(256) void k_hexconv_stream(const Tin* __restrict__ 
                     ap = __builtin_elementwise_fma(wp2[o * 7 + t], UP[sl][dk], ap);
                     as = fmaf(wk[o * 7 + t], U[sl][dk][0], as);
                 }
-                if (own) cs_store<Tout>(from_acc<Tout>((ap.x + ap.y) + as), yrs[o], obytecol, ob);
+                float v = (ap.x + ap.y) + as;
+                if (F.epi.on) v = epi_apply(v, o, F.epi);
+                if (own) cs_store<Tout>(from_acc<Tout>(v), yrs[o], obytecol, ob);
             }
         } else {
 #pragma unroll
@@ -221,6 +224,7 @@ __global__ __launch_bounds__(256) void k_hexconv_stream(const Tin* __restrict__ 
                         acc = fmaf(wk[(o * CG + ci) * 7 + t],
                                    U[SLT[cs_tap_ii(t)]][cs_tap_dk(t, PAR, OP)][c], acc);
                 }
+                if (F.epi.on) acc = epi_apply(acc, o, F.epi);
                 if (own) cs_store<Tout>(from_acc<Tout>(acc), yrs[o], obytecol, ob);
             }
         }
@@ -282,11 +286,13 @@ static int cs_channels(const void* x, const float* k, const float* b, void* y,
 // stride 1, dilation 1, constant padding, float32 weights.
 int launch_conv_stream(const void* x, const float* k, const float* b, void* y, int x_dtype,
                        int y_dtype, int64_t B, int C, int O, int64_t h, int64_t w, int p,
-                       int groups, int off, double pad_value, hipStream_t st) {
+                       int groups, int off, double pad_value, const Epilogue& epi,
+                       hipStream_t st) {
     if (p < 0 || p > 2 || h > INT_MAX / 4 || w > INT_MAX / 4) return HG_EUNSUP;
     if (h * w * 8 >= INT_MAX) return HG_EUNSUP;   // 32-bit buffer offsets
     ConvStreamGeom F;
     F.B = B; F.h = (int)h; F.w = (int)w; F.p = p; F.padv = (float)pad_value;
+    F.epi = epi;
     F.ho = F.h + 2 * p - 2;
     F.wo = F.w + 2 * p - 2;
     if (F.ho < 1 || F.wo < 1) return HG_EUNSUP;

@@ -40,6 +40,7 @@ struct ConvGeom {
     int nPr, pitch;   // LDS footprint rows / pitch (elements)
     int mink;         // min column tap offset over both parities
     double pad_value;
+    Epilogue epi;
 };
 
 template <typename Tin, typename Tout, typename A, int OCB, int KFIX>
@@ -145,7 +146,9 @@ __global__ __launch_bounds__(CV_THREADS) void k_hexconv(const Tin* __restrict__ 
 #pragma unroll
                         for (int k = 0; k < CV_RPT; ++k) {
                             const int64_t ro = r0 + lr0 + k;
-                            if (ro < G.ho) yp[ro * G.wo + q] = from_acc<Tout>(acc[k][j]);
+                            A v = acc[k][j];
+                            if (G.epi.on) v = epi_apply(v, g * G.og + oc0 + j, G.epi);
+                            if (ro < G.ho) yp[ro * G.wo + q] = from_acc<Tout>(v);
                         }
                     }
                 }
@@ -188,6 +191,7 @@ __global__ __launch_bounds__(256) void k_hexconv_direct(const Tin* __restrict__ 
             acc += wv * v;
         }
     }
+    if (G.epi.on) acc = epi_apply(acc, (int)o, G.epi);
     y[idx] = from_acc<Tout>(acc);
 }
 
@@ -232,7 +236,8 @@ static int conv_dispatch(const void* x, const void* k, const void* b, void* y,
 
 int launch_conv_stream(const void* x, const float* k, const float* b, void* y, int x_dtype,
                        int y_dtype, int64_t B, int C, int O, int64_t h, int64_t w, int p,
-                       int groups, int off, double pad_value, hipStream_t st);   // conv_stream.hip
+                       int groups, int off, double pad_value, const Epilogue& epi,
+                       hipStream_t st);   // conv_stream.hip
 
 }  // namespace hg
 
@@ -249,7 +254,24 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
                  int64_t out_channels, int64_t h, int64_t w, int radius, int stride,
                  int padding, int dilation, int groups, int even_odd_offset, int pad_mode,
                  double pad_value, void* stream) {
+    return hg_hexconv2d_epilogue(x, kernel, bias, y, x_dtype, w_dtype, y_dtype, batch,
+                                 in_channels, out_channels, h, w, radius, stride, padding,
+                                 dilation, groups, even_odd_offset, pad_mode, pad_value, nullptr,
+                                 nullptr, HG_ACT_NONE, 0.0, stream);
+}
+
+int hg_hexconv2d_epilogue(const void* x, const void* kernel, const void* bias, void* y,
+                          int x_dtype, int w_dtype, int y_dtype, int64_t batch,
+                          int64_t in_channels, int64_t out_channels, int64_t h, int64_t w,
+                          int radius, int stride, int padding, int dilation, int groups,
+                          int even_odd_offset, int pad_mode, double pad_value,
+                          const void* scale, const void* shift, int act, double act_param,
+                          void* stream) {
     using namespace hg;
+    if (act < HG_ACT_NONE || act > HG_ACT_TANH) return HG_EINVAL;
+    Epilogue epi;
+    epi.scale = scale; epi.shift = shift; epi.act = act; epi.slope = act_param;
+    epi.on = (scale || shift || act != HG_ACT_NONE) ? 1 : 0;
     ConvGeom G;
     int st = conv_out_shape(h, w, radius, stride, padding, dilation, &G.ho, &G.wo);
     if (st) return st;
@@ -268,12 +290,13 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
         // register-streaming fast path (conv_stream.hip); EUNSUP -> generic kernel
         st = launch_conv_stream(x, (const float*)kernel, (const float*)bias, y, x_dtype, y_dtype,
                                 batch, (int)in_channels, (int)out_channels, h, w, padding,
-                                groups, even_odd_offset & 1, pad_value, s);
+                                groups, even_odd_offset & 1, pad_value, epi, s);
         if (st != HG_EUNSUP) return st;
     }
     G.B = batch; G.C = in_channels; G.O = out_channels; G.h = h; G.w = w;
     G.r = radius; G.s = stride; G.p = padding; G.d = dilation; G.groups = groups;
     G.off = even_odd_offset & 1; G.pad_mode = pad_mode; G.pad_value = pad_value;
+    G.epi = epi;
     G.cg = (int)(in_channels / groups);
     G.og = (int)(out_channels / groups);
     G.ntx = (int)((G.wo + CV_TC - 1) / CV_TC);

@@ -44,6 +44,12 @@ enum hg_interp { HG_NEAREST = 0, HG_LINEAR = 1 };
 enum hg_pad_mode { HG_PAD_CONSTANT = 0, HG_PAD_REFLECT = 1, HG_PAD_REPLICATE = 2,
                    HG_PAD_CIRCULAR = 3 };
 
+/* Activations of the fused HexConv2d epilogue (hg_hexconv2d_epilogue): the act layers
+ * HexConvModule builds (HexModules.py:229-236, mmcv ReLU / LeakyReLU / ReLU6 / Sigmoid /
+ * Tanh). */
+enum hg_act { HG_ACT_NONE = 0, HG_ACT_RELU = 1, HG_ACT_LEAKY_RELU = 2, HG_ACT_RELU6 = 3,
+              HG_ACT_SIGMOID = 4, HG_ACT_TANH = 5 };
+
 /* Lattice-map operation codes for hg_lattice_maps. */
 enum hg_op { HG_OP_RECT_TO_HEX = 0, HG_OP_HEX_TO_RECT = 1, HG_OP_HEXRESIZE = 2 };
 
@@ -115,6 +121,22 @@ int hg_hexconv2d(const void* x, const void* kernel, const void* bias, void* y, i
                  int64_t out_channels, int64_t h, int64_t w, int radius, int stride,
                  int padding, int dilation, int groups, int even_odd_offset, int pad_mode,
                  double pad_value, void* stream);
+
+/* hg_hexconv2d with a fused per-output-channel epilogue: replaces HexConvModule's
+ * conv -> norm -> act sequence (HexModules.py:258-268) when the norm is an affine map
+ * (BatchNorm in eval mode, folded by the caller into scale = gamma / sqrt(var + eps),
+ * shift = beta - mean * scale) or absent:
+ *     y[b, o] = act(scale[o] * (conv + bias[o]) + shift[o]),
+ * scale / shift: (O,) of w_dtype, either may be NULL (1 / 0); act: hg_act;
+ * act_param: the LeakyReLU negative slope.  One pass: the norm and activation never
+ * re-read the conv output from HBM. */
+int hg_hexconv2d_epilogue(const void* x, const void* kernel, const void* bias, void* y,
+                          int x_dtype, int w_dtype, int y_dtype, int64_t batch,
+                          int64_t in_channels, int64_t out_channels, int64_t h, int64_t w,
+                          int radius, int stride, int padding, int dilation, int groups,
+                          int even_odd_offset, int pad_mode, double pad_value,
+                          const void* scale, const void* shift, int act, double act_param,
+                          void* stream);
 
 /* HexConv2d backward: gradients of hg_hexconv2d for an upstream gradient gy
  * (B, O, ho, wo) of w_dtype.  Replaces the reference's autograd path through
