@@ -71,6 +71,9 @@ constexpr int FU_LUT = FU_RB + 2;     // u rows band_begin-1 .. band_begin+RB
 #ifndef FU_L12
 #define FU_L12 1                      // 12-step loop body (two 6-step blocks per trip)
 #endif
+#ifndef FU_MIN_INST
+#define FU_MIN_INST 0                 // 1: build only the bf16 C3 O3 G1 kernels (variants)
+#endif
 #ifndef FU_DRAIN
 #define FU_DRAIN 1                    // drain the prologue's loads before the row loop
 #endif
@@ -591,6 +594,11 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
     F.rys = g.ys;
     F.nwin = (int)((w2 + FU_OWN - 1) / FU_OWN);
     F.nband = (int)((h2 + FU_RB - 1) / FU_RB);
+#if FU_MIN_INST   // tuning variants: only the headline instantiation (fast rebuilds)
+    if (x_dtype == HG_BF16 && y_dtype == HG_BF16 && C == 3 && O == 3 && G == 1)
+        return fused_launch<__bf16, __bf16, 3, 3, 1>(x, kernel, bias, y, F, op, st);
+    return HG_EUNSUP;
+#endif
     switch (x_dtype) {
     case HG_BF16:
         switch (y_dtype) {

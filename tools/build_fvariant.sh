@@ -9,8 +9,8 @@ NAME=$1; shift
 OBJ=$PKG/build/obj
 OUT=$PKG/HyGrid/_lib/variants
 mkdir -p "$OUT" "$OBJ/variants"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -DFU_MIN_INST=1 "$@" \
     -I"$PKG/csrc" -c "${FUSED_SRC:-$PKG/csrc/fused.hip}" -o "$OBJ/variants/fused_$NAME.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libhygrid_$NAME.so" \
-    "$OBJ/abi.o" "$OBJ/resample.o" "$OBJ/hexconv.o" "$OBJ/conv_stream.o" "$OBJ/pipeline.o" "$OBJ/variants/fused_$NAME.o"
+    $(ls "$OBJ"/*.o | grep -v '/fused.o$') "$OBJ/variants/fused_$NAME.o"
 echo "$OUT/libhygrid_$NAME.so"

@@ -46,6 +46,8 @@ __global__ __launch_bounds__(256) void k(float* out, int iters, float sv, unsign
             if (MODE == 28) asm volatile("v_max_f32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(a[(i + 2) & 7]));
             if (MODE == 29) asm volatile("v_cvt_f32_bf16 %0, %1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
             if (MODE == 30) asm volatile("v_cvt_f32_bf16_sdwa %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1" : "=v"(a[i]) : "v"(a[(i + 3) & 7]));
+            if (MODE == 31) asm volatile("v_fmac_f32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a[i]) : "v"(a[(i + 3) & 7]), "v"(m));
+            if (MODE == 32) { float t; asm volatile("v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(t) : "v"(a[(i + 3) & 7])); asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(a[i]) : "v"(t), "v"(m)); }
             if (MODE == 6) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[i]) : "s"(sv), "v"(a[(i + 1) & 7]));
         }
     }
@@ -56,8 +58,8 @@ __global__ __launch_bounds__(256) void k(float* out, int iters, float sv, unsign
 }
 
 template <int MODE>
-void run(const char* name, float* o, unsigned long long* clk) {
-    const int blocks = 1024 * 8, iters = 2048;   // 32 waves per CU = 8 per SIMD
+void run(const char* name, float* o, unsigned long long* clk, int wps) {
+    const int blocks = 256 * wps, iters = 2048;   // wps waves per SIMD (4 waves per block)
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     hipLaunchKernelGGL(k<MODE>, dim3(blocks), dim3(256), 0, 0, o, iters, 0.5f, clk);
     CK(hipDeviceSynchronize());
@@ -69,25 +71,24 @@ void run(const char* name, float* o, unsigned long long* clk) {
     CK(hipMemcpy(hc.data(), clk, hc.size() * 8, hipMemcpyDeviceToHost));
     double cy = 0, rt = 0; for (int i = 0; i < blocks; ++i) { cy += hc[2 * i]; rt += hc[2 * i + 1]; }
     const double ghz = cy / rt * 0.1;
-    const double waves_per_simd = blocks * 4.0 / 1024;
-    printf("%-28s %.3f ms  %.2f GHz  %.2f cycles/wave-instr/SIMD\n", name, ms, ghz,
-           ms * 1e-3 * ghz * 1e9 / (waves_per_simd * 8.0 * iters));
+    printf("%-30s wps %d  %.3f ms  %.2f GHz  %.2f cycles/wave-instr/SIMD\n", name, wps, ms, ghz,
+           ms * 1e-3 * ghz * 1e9 / ((double)wps * 8.0 * iters));
 }
 
 int main() {
     float* o; unsigned long long* clk;
     CK(hipMalloc(&o, (size_t)1024 * 8 * 256 * 4)); CK(hipMalloc(&clk, (size_t)1024 * 8 * 16));
-    run<0>("v_fmac_f32 v,v", o, clk);
-    run<20>("v_perm_b32", o, clk);
-    run<21>("v_alignbyte_b32 ,2", o, clk);
-    run<22>("v_lshlrev_b32 v,v", o, clk);
-    run<23>("v_lshlrev_b32_sdwa", o, clk);
-    run<24>("v_mov_b32_sdwa WORD_1<-WORD_0", o, clk);
-    run<25>("v_cndmask_b32 vcc", o, clk);
-    run<26>("v_permlane32_swap", o, clk);
-    run<27>("v_cvt_f32_f16", o, clk);
-    run<28>("v_max_f32", o, clk);
-    run<29>("v_cvt_f32_bf16", o, clk);
-    run<30>("v_cvt_f32_bf16_sdwa WORD_1", o, clk);
+    for (int w : {1, 2, 3, 4, 8}) {
+        run<0>("v_fmac_f32 v,v(m)", o, clk, w);
+        run<12>("v_fmac_f32 v,v,v", o, clk, w);
+        run<1>("v_fmac_f32 s,v", o, clk, w);
+        run<2>("v_mov_b32_dpp wave_shr", o, clk, w);
+        run<4>("v_mul_f32_dpp wave_shr", o, clk, w);
+        run<31>("v_fmac_f32_dpp wave_shr", o, clk, w);
+        run<32>("dpp mov then dependent fmac", o, clk, w);
+        run<9>("v_dot2c_f32_bf16", o, clk, w);
+        run<19>("v_pk_fma_f32", o, clk, w);
+        run<11>("v_cvt_pk_bf16_f32", o, clk, w);
+    }
     return 0;
 }
