@@ -57,6 +57,9 @@ def parse():
                     help="time the three operators (r2h, HexConv2d, h2r) instead of the fused kernel")
     ap.add_argument("--no-compare", action="store_true",
                     help="skip the secondary (unfused) measurement in the fused run")
+    ap.add_argument("--no-pyramid", action="store_true",
+                    help="skip the secondary config-5 line (8K fp16 3-level hex pyramid)")
+    ap.add_argument("--pyramid-batch", type=int, default=8, help="8K images per GPU (config 5)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-kernel HBM bytes from rocprofv3 PMC passes (optional)")
     return ap.parse_args()
@@ -187,7 +190,10 @@ def main():
             log("pmc json unreadable:", exc)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "alg_bytes_per_launch": alg_bytes[dom]}
+                "traffic": traffic, "alg_bytes_per_launch": alg_bytes[dom],
+                "limiter": "VALU issue for the fused kernel: a build whose loads/stores hit one "
+                           "cache-resident row runs as fast (DESIGN.md section 9)"
+                if dom == "pipeline_r2h_conv_h2r" else "hbm"}
 
     compare = None
     if not args.unfused and not args.no_compare:
@@ -201,6 +207,55 @@ def main():
                    "kernels": {k: {"ms": round(m, 4),
                                    "GB_per_s": round(2 * img_bytes / (m * 1e-3) / 1e9, 1)}
                                for k, m in zip(ks, sms_u)}}
+
+    pyramid = None
+    if not args.unfused and not args.no_pyramid:
+        # BASELINE configs[4], per GPU: 8K fp16 rasters, r2h at full
+        # size, then 3 x [depthwise HexConv2d(3,3,0,2,padding=1,groups=3) with Gaussian
+        # taps [1,1,1,6,1,1,1]/12 -> hexresize to (h//2, w//2)].  Reported beside
+        # `value`, never as it.
+        f16 = torch.float16
+        Hp, Wp, Bp = 4320, 7680, args.pyramid_batch
+        xp = torch.rand((Bp, C, Hp, Wp), generator=gen, device=dev, dtype=f16)
+        gconv = HexConv2d(C, C, 0, 2, padding=1, groups=C, bias=False).to(dev)
+        with torch.no_grad():
+            gconv.kernel.copy_(torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32,
+                                            device=dev).div_(12).expand_as(gconv.kernel))
+        gconv.out_dtype = f16
+        levels = []
+
+        def run_pyramid(record, ev):
+            if record:
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(8)]
+                e[0].record()
+            hx = ops.rect_to_hex(xp, (Hp, Wp), out_dtype=f16)
+            if record:
+                e[1].record()
+            h_, w_ = Hp, Wp
+            for lv in range(3):
+                hx = gconv(hx)
+                if record:
+                    e[2 + 2 * lv].record()
+                h_, w_ = h_ // 2, w_ // 2
+                hx = ops.hexresize(hx, (h_, w_), out_dtype=f16)
+                if record:
+                    e[3 + 2 * lv].record()
+            if record:
+                ev.append(e)
+            if not levels:
+                levels.append(tuple(hx.shape))
+            return hx
+
+        steps_p = max(2, args.steps // 2)
+        _, el_p, sms_p = measure(run_pyramid, steps_p, 1)
+        names = ["rect_to_hex"] + [f"{k}_l{lv}" for lv in range(3) for k in ("hexconv_dw", "hexresize")]
+        pyramid = {"workload": "config5: 8K RGB fp16, r2h -> 3 x [depthwise Gaussian HexConv2d "
+                               "-> hexresize /2]",
+                   "batch_per_gpu": Bp, "value": round(world * Bp * Hp * Wp * steps_p / el_p / 1e6, 1),
+                   "unit": "Mpix/s", "ms_per_step": round(el_p / steps_p * 1e3, 4),
+                   "dtype": "f16", "out_shape": list(levels[0]),
+                   "kernels_ms": {k: round(m, 4) for k, m in zip(names, sms_p)}}
+        del xp
 
     # checksums over RCCL (not timed), and the full-output gather on its own
     from HyGrid.dist import gather_checksums, gather_to_root, image_checksums
@@ -249,7 +304,7 @@ def main():
                        "height": H, "width": W, "parallelism": f"dp{world}",
                        "fused": not args.unfused},
             "kernels": kernels, "roofline": roofline, "cpu_baseline": cpu,
-            "unfused": compare, "gather": gather, "checksum": checksum,
+            "unfused": compare, "pyramid": pyramid, "gather": gather, "checksum": checksum,
             "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)

@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "lattice.h"
+#include "stream.h"
 
 namespace hg {
 
@@ -496,6 +497,10 @@ static int resample(const void* src, void* dst, int sdt, int ddt, int64_t planes
     if (interp != HG_LINEAR) return HG_EINVAL;
     if (!dtype_is_float(ddt)) return HG_EDTYPE;
     const bool dbl = acc_is_double(sdt, ddt);
+    if (!dbl && OP != OP_RESIZE) {   // near-identity lattices: row-streaming kernels
+        const int rc = stream_try(OP, src, dst, sdt, ddt, planes, h, w, h1, w1, s);
+        if (rc != HG_EUNSUP) return rc;
+    }
     HG_DISPATCH_IN(sdt, TIN, HG_DISPATCH_FLOAT_OUT(ddt, TOUT, {
         if (dbl) return launch_linear<OP, TIN, TOUT, double>(src, dst, planes, g, s);
         return launch_linear<OP, TIN, TOUT, float>(src, dst, planes, g, s);

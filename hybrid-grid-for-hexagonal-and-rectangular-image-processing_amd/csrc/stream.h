@@ -1,0 +1,15 @@
+// stream.h — row-streaming resample kernels for near-identity lattices
+// (resample_stream.hip), tried first by hg_rect_to_hex / hg_hex_to_rect (resample.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hg {
+
+// Runs the streaming kernel if the call is in its domain (r2h with a near-identity
+// lattice, h2r at the same size; 16/32-bit float in and out; widths a multiple of 4);
+// returns HG_EUNSUP (nothing launched) otherwise.  Bit-identical to the general kernels.
+int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h,
+               int64_t w, int64_t h1, int64_t w1, hipStream_t st);
+
+}  // namespace hg
