@@ -90,7 +90,7 @@ __device__ __forceinline__ A blend(A v0, A v1, A v2, A v3, A c0, A c1, A c2, A f
 
 template <typename T> struct VecOf { static constexpr int N = 16 / (int)sizeof(T); };
 
-constexpr int RS_MAXPF = 4;   // 16-byte staging chunks held in registers per thread
+constexpr int RS_MAXPF = 8;   // 16-byte staging chunks held in registers per thread
 
 // Load this thread's chunks of one plane's footprint (raw bits, zeros outside).
 template <typename Tin>
