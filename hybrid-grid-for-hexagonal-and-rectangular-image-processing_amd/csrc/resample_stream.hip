@@ -114,6 +114,12 @@ __device__ __forceinline__ float st_next(float v, float old) {
         __builtin_bit_cast(int, old), __builtin_bit_cast(int, v), 0x130 /*wave_shl:1*/, 0xf, 0xf, false));
 }
 
+// one source row as seen by a lane: its 4 columns and the window-edge dword halves
+struct StRow {
+    float v[4], el, eh;
+    __device__ __forceinline__ void zero() { v[0] = v[1] = v[2] = v[3] = el = eh = 0.f; }
+};
+
 struct WaveUnit {
     int64_t plane;
     int win, s0, s1;
@@ -201,7 +207,18 @@ __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict
     const unsigned xrow = (unsigned)S.w * (unsigned)sizeof(Tin);
     const unsigned yrow = (unsigned)S.w1 * (unsigned)sizeof(Tout);
 
-    auto row = [&](int r) {
+    // Register ring of source rows: every row is loaded once (one main + one edge load);
+    // rows outside the raster read as zeros (:478-486), so the taps of a row with
+    // in(r) - r in {-1, 0} need no further masking.
+    auto load_row = [&](int rr, StRow& R) {
+        const unsigned so = (unsigned)min(max(rr, 0), S.h - 1) * xrow;
+        st_load4<Tin>(xrs, xoff, so, R.v);
+        st_load_edge<Tin>(xrs, eoff, so, &R.el, &R.eh);
+        if (rr < 0 || rr >= S.h) R.zero();            // uniform
+    };
+    // output row r from source rows r-1, r, r+1
+    auto row = [&](int r, const StRow& Rm, const StRow& Rc, const StRow& Rp) {
+        if (r >= u.s1) return;                        // uniform (last trip of a band)
         const int e = r - u.s0, k = e >> 6, l = e & 63;
         const int in = __builtin_amdgcn_readlane(k ? rin[1] : rin[0], l);
         const float c0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
@@ -209,23 +226,18 @@ __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict
         const float c1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
             __builtin_bit_cast(int, k ? rc1[1] : rc1[0]), l));
         const unsigned val = (unsigned)__builtin_amdgcn_readlane((int)(k ? rval[1] : rval[0]), l);
-        const unsigned soA = (unsigned)min(max(in, 0), S.h - 1) * xrow;
-        const unsigned soB = (unsigned)min(max(in + 1, 0), S.h - 1) * xrow;
-        float A[4], B[4], Al, Ah, Bl, Bh;
-        st_load4<Tin>(xrs, xoff, soA, A);
-        st_load4<Tin>(xrs, xoff, soB, B);
-        st_load_edge<Tin>(xrs, eoff, soA, &Al, &Ah);
-        st_load_edge<Tin>(xrs, eoff, soB, &Bl, &Bh);
-        if (!(val & 1u)) { A[0] = A[1] = A[2] = A[3] = Al = Ah = 0.f; }   // row outside: taps 0
-        if (!(val & 2u)) { B[0] = B[1] = B[2] = B[3] = Bl = Bh = 0.f; }
+        const bool up = in != r;                      // in == r - 1 (else in == r)
+        StRow A = up ? Rm : Rc, B = up ? Rc : Rp;     // rows in, in + 1
+        if (!(val & 1u)) A.zero();                    // a dead row (no live tap): all zero
+        if (!(val & 2u)) B.zero();
         // vertical blend per column, t = c0 * P(in+1) + c1 * P(in)   (:515-516)
         float t[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] = c0 * B[c] + c1 * A[c];
-        const float tl = c0 * Bh + c1 * Ah;       // column W0-1 (meaningful on lane 0)
-        const float tr = c0 * Bl + c1 * Al;       // column W0+256 (lane 63)
-        const float tm = st_prev(t[3], tl);       // column ce - 1
-        const float tp = st_next(t[0], tr);       // column ce + 4
+        for (int c = 0; c < 4; ++c) t[c] = c0 * B.v[c] + c1 * A.v[c];
+        const float tl = c0 * B.eh + c1 * A.eh;       // column W0-1 (meaningful on lane 0)
+        const float tr = c0 * B.el + c1 * A.el;       // column W0+256 (lane 63)
+        const float tm = st_prev(t[3], tl);           // column ce - 1
+        const float tp = st_next(t[0], tr);           // column ce + 4
         float o[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -237,11 +249,24 @@ __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict
         }
         st_store4<Tout>(o, yrs, yoff, (unsigned)r * yrow);
     };
-    // four rows per trip (their loads issue together); readlane is convergent, so the
-    // compiler will not unroll a runtime-count loop around it by itself
-    int r = u.s0;
-    for (; r + 4 <= u.s1; r += 4) { row(r); row(r + 1); row(r + 2); row(r + 3); }
-    for (; r < u.s1; ++r) row(r);
+    // four output rows per trip: four new source rows (r0+1 .. r0+4) issue together;
+    // readlane is convergent, so the compiler would not unroll this loop by itself
+    StRow P0, P1;
+    load_row(u.s0 - 1, P0);
+    load_row(u.s0, P1);
+    for (int r0 = u.s0; r0 < u.s1; r0 += 4) {
+        StRow N0, N1, N2, N3;
+        load_row(r0 + 1, N0);
+        load_row(r0 + 2, N1);
+        load_row(r0 + 3, N2);
+        load_row(r0 + 4, N3);
+        row(r0, P0, P1, N0);
+        row(r0 + 1, P1, N0, N1);
+        row(r0 + 2, N0, N1, N2);
+        row(r0 + 3, N1, N2, N3);
+        P0 = N2;
+        P1 = N3;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -267,43 +292,51 @@ __global__ __launch_bounds__(ST_THREADS) void k_h2r_stream(const Tin* __restrict
     const unsigned xrow = (unsigned)S.w * (unsigned)sizeof(Tin);
     const unsigned yrow = (unsigned)S.w * (unsigned)sizeof(Tout);
 
-    auto row = [&](int a, auto ODDc) {
+    auto load_row = [&](int rr, StRow& R) {       // ring row; zeros outside the raster
+        const unsigned so = (unsigned)min(rr, S.h - 1) * xrow;
+        st_load4<Tin>(xrs, xoff, so, R.v);
+        st_load_edge<Tin>(xrs, eoff, so, &R.el, &R.eh);
+        if (rr >= S.h) R.zero();                      // uniform
+    };
+    // output row a from hex rows a (Z) and a + 1 (N; zero below the raster, :303-323)
+    auto row = [&](int a, auto ODDc, const StRow& Z, const StRow& N) {
         constexpr bool odd = decltype(ODDc)::value;
-        const float al = odd ? S.tri[1][0] : S.tri[0][0];
-        const float be = odd ? S.tri[1][1] : S.tri[0][1];
-        const float ga = odd ? S.tri[1][2] : S.tri[0][2];
-        const bool below = a + 1 < S.h;           // p3's row inside the raster
-        float Z[4], N[4], el, eh;
-        st_load4<Tin>(xrs, xoff, (unsigned)a * xrow, Z);
-        st_load4<Tin>(xrs, xoff, (unsigned)(below ? a + 1 : a) * xrow, N);
-        st_load_edge<Tin>(xrs, eoff, (unsigned)a * xrow, &el, &eh);
-        if (!below) { N[0] = N[1] = N[2] = N[3] = 0.f; }
+        if (a >= u.s1) return;                        // uniform (last trip of a band)
+        const float al = S.tri[odd][0], be = S.tri[odd][1], ga = S.tri[odd][2];
         float o[4];
-        if constexpr (!odd) {                     // p1 = (a, b), p2 = (a, b+1)
-            const float zp = st_next(Z[0], el);   // column ce + 4
+        if constexpr (!odd) {                         // p1 = (a, b), p2 = (a, b+1)
+            const float zp = st_next(Z.v[0], Z.el);   // column ce + 4
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                const float p2 = c == 3 ? zp : Z[c + 1];
-                o[c] = al * Z[c] + be * p2 + ga * N[c];   // :354
+                const float p2 = c == 3 ? zp : Z.v[c + 1];
+                o[c] = al * Z.v[c] + be * p2 + ga * N.v[c];   // :354
             }
-        } else {                                  // p1 = (a, b-1), p2 = (a, b)
-            const float zm = st_prev(Z[3], eh);   // column ce - 1
+        } else {                                      // p1 = (a, b-1), p2 = (a, b)
+            const float zm = st_prev(Z.v[3], Z.eh);   // column ce - 1
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                const float p1 = c == 0 ? zm : Z[c - 1];
-                o[c] = al * p1 + be * Z[c] + ga * N[c];
+                const float p1 = c == 0 ? zm : Z.v[c - 1];
+                o[c] = al * p1 + be * Z.v[c] + ga * N.v[c];
             }
         }
         st_store4<Tout>(o, yrs, yoff, (unsigned)a * yrow);
     };
-    // bands start on even rows (ST_RB is even): four rows per trip, parity static
-    int a = u.s0;
-    for (; a + 4 <= u.s1; a += 4) {
-        row(a, std::false_type{}); row(a + 1, std::true_type{});
-        row(a + 2, std::false_type{}); row(a + 3, std::true_type{});
+    // bands start on even rows (ST_RB is even): four rows per trip, parity static,
+    // every hex row loaded once
+    StRow P;
+    load_row(u.s0, P);
+    for (int a = u.s0; a < u.s1; a += 4) {
+        StRow N0, N1, N2, N3;
+        load_row(a + 1, N0);
+        load_row(a + 2, N1);
+        load_row(a + 3, N2);
+        load_row(a + 4, N3);
+        row(a, std::false_type{}, P, N0);
+        row(a + 1, std::true_type{}, N0, N1);
+        row(a + 2, std::false_type{}, N1, N2);
+        row(a + 3, std::true_type{}, N2, N3);
+        P = N3;
     }
-    for (; a + 2 <= u.s1; a += 2) { row(a, std::false_type{}); row(a + 1, std::true_type{}); }
-    if (a < u.s1) row(a, std::false_type{});
 }
 
 // ---------------------------------------------------------------------------
