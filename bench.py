@@ -257,6 +257,37 @@ def main():
                    "kernels_ms": {k: round(m, 4) for k, m in zip(names, sms_p)}}
         del xp
 
+    roundtrip = None
+    if not args.unfused and not args.no_pyramid:
+        # BASELINE configs[1]: 1080p RGB fp32, batch 32 per GPU,
+        # rect->hex bilinear -> hex->rect linear.  Reported beside `value`, never as it.
+        Hr, Wr, Br = 1080, 1920, 32
+        xr = torch.rand((Br, C, Hr, Wr), generator=gen, device=dev, dtype=torch.float32)
+
+        def run_roundtrip(record, ev):
+            if record:
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                e[0].record()
+            hx = ops.rect_to_hex(xr, (Hr, Wr))
+            if record:
+                e[1].record()
+            out = ops.hex_to_rect(hx, (Hr, Wr))
+            if record:
+                e[2].record()
+                ev.append(e)
+            return out
+
+        steps_r = max(2, args.steps // 2)
+        _, el_r, sms_r = measure(run_roundtrip, steps_r, 1)
+        tb = Br * C * Hr * Wr * 4 * 2                 # each kernel: read once + write once
+        roundtrip = {"workload": "config2: 1080p RGB fp32, rect->hex bilinear -> hex->rect linear",
+                     "batch_per_gpu": Br, "dtype": "f32",
+                     "value": round(world * Br * Hr * Wr * steps_r / el_r / 1e6, 1),
+                     "unit": "Mpix/s", "ms_per_step": round(el_r / steps_r * 1e3, 4),
+                     "kernels": {k: {"ms": round(m, 4), "GB_per_s": round(tb / (m * 1e-3) / 1e9, 1)}
+                                 for k, m in zip(("rect_to_hex", "hex_to_rect"), sms_r)}}
+        del xr
+
     # checksums over RCCL (not timed), and the full-output gather on its own
     from HyGrid.dist import gather_checksums, gather_to_root, image_checksums
     cs = image_checksums(y)
@@ -304,7 +335,7 @@ def main():
                        "height": H, "width": W, "parallelism": f"dp{world}",
                        "fused": not args.unfused},
             "kernels": kernels, "roofline": roofline, "cpu_baseline": cpu,
-            "unfused": compare, "pyramid": pyramid, "gather": gather, "checksum": checksum,
+            "unfused": compare, "roundtrip": roundtrip, "pyramid": pyramid, "gather": gather, "checksum": checksum,
             "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)

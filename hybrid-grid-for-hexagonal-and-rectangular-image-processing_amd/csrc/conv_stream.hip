@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "fused.h"
 
 namespace hg {
 
@@ -289,6 +290,11 @@ int launch_conv_stream(const void* x, const float* k, const float* b, void* y, i
                        int groups, int off, double pad_value, const Epilogue& epi,
                        hipStream_t st) {
     if (p < 0 || p > 2 || h > INT_MAX / 4 || w > INT_MAX / 4) return HG_EUNSUP;
+    {   // two-column streaming kernel (fused_conv.hip) where it applies
+        const int rc = fused_conv_try(x, k, b, y, x_dtype, y_dtype, B, C, O, groups, h, w, p, off,
+                                      pad_value, epi.on != 0, st);
+        if (rc != HG_EUNSUP) return rc;
+    }
     if (h * w * 8 >= INT_MAX) return HG_EUNSUP;   // 32-bit buffer offsets
     ConvStreamGeom F;
     F.B = B; F.h = (int)h; F.w = (int)w; F.p = p; F.padv = (float)pad_value;

@@ -1,0 +1,527 @@
+// fused_kernel.h — the two-column streaming kernel shared by the fused pipeline
+// (fused.hip: rect -> hex -> HexConv2d(r=2) -> hex -> rect) and the HexConv2d-only
+// mode (fused_conv.hip).  See fused.hip for the pipeline's design notes.
+#pragma once
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+#include "fused.h"
+#include "lattice.h"
+
+namespace hg {
+
+constexpr int FU_THREADS = 256;       // 4 independent waves per workgroup
+constexpr int FU_HL = 4;              // halo columns on the left of a window
+constexpr int FU_OWN = 120;           // owned columns per 128-column window
+constexpr int FU_RB = 126;            // output rows per band (multiple of 6)
+constexpr int FU_LUT = FU_RB + 2;     // u rows band_begin-1 .. band_begin+RB
+
+// Tuning knobs (compile-time; tools/build_fvariant.sh builds variants of this file).
+#ifndef FU_PD
+#define FU_PD 3                       // rect rows loaded ahead of use (1..4)
+#endif
+#ifndef FU_WPE
+#define FU_WPE 1                      // minimum waves per SIMD asked of the register allocator
+#endif
+#ifndef FU_WPE_CONV
+#define FU_WPE_CONV 4                 // HexConv2d mode: 129 -> 128 VGPRs buys a 4th wave per SIMD
+#endif
+#ifndef FU_NOMEM
+#define FU_NOMEM 0                    // diagnostic: every row load / store hits row 0 (cache-resident)
+#endif
+#ifndef FU_WSGPR
+#define FU_WSGPR 0                    // 1: conv weights in SGPRs (uniform loads) instead of VGPRs
+#endif
+#ifndef FU_STAGE
+#define FU_STAGE 0                    // 16-bit outputs: stage rows in LDS, store whole 128-B lines
+#endif
+#ifndef FU_SCHED
+#define FU_SCHED 0                    // 1: scheduling barrier between steps (bounds register use)
+#endif
+#ifndef FU_CD
+#define FU_CD 1                       // per-wave column-class specialisation of the r2h taps
+#endif
+#ifndef FU_L12
+#define FU_L12 1                      // 12-step loop body (two 6-step blocks per trip)
+#endif
+#ifndef FU_MIN_INST
+#define FU_MIN_INST 0                 // 1: build only the bf16 C3 O3 G1 kernels (variants)
+#endif
+#ifndef FU_DRAIN
+#define FU_DRAIN 1                    // drain the prologue's loads before the row loop
+#endif
+
+struct FusedGeom {
+    int64_t B;
+    int h, w, h1, w1, h2, w2;
+    int nwin, nband;
+    Axis rxs, rys;                    // r2h lattice axes (geometry_np.py:415-422)
+};
+
+__device__ __forceinline__ float f_prev(float v) {   // result[l] = v[l-1], 0 at lane 0
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+        __builtin_bit_cast(int, v), 0x138 /*wave_shr:1*/, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float f_next(float v) {   // result[l] = v[l+1], 0 at lane 63
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+        __builtin_bit_cast(int, v), 0x130 /*wave_shl:1*/, 0xf, 0xf, true));
+}
+
+// r=2 stencil taps (HexFrames.py:108-118 scatter into the dense 3x5 kernel):
+// row of tap t relative to the output row (0 above, 1 centre, 2 below) and its lane
+// column shift for an output row of parity `par` (type1 indexing, :417-445; derived in
+// oracle/hg_oracle.c), with padding 1: shift = dk - 1.
+__host__ __device__ constexpr int fu_tap_ii(int t) { return t < 2 ? 0 : (t < 5 ? 1 : 2); }
+__host__ __device__ constexpr int fu_tap_col(int t) {
+    return t < 2 ? 1 + 2 * t : (t < 5 ? 2 * (t - 2) : 1 + 2 * (t - 5));
+}
+__host__ __device__ constexpr int fu_tap_shift(int t, int par, int op) {
+    return ((1 + par + fu_tap_col(t) - ((((par + fu_tap_ii(t)) & 1) + op) & 1)) >> 1) - 1;
+}
+
+template <typename T> struct RawOf { using type = unsigned; };          // 2 x 16-bit
+template <> struct RawOf<float> { using type = uint2; };                // 2 x f32
+
+template <typename T>
+__device__ __forceinline__ typename RawOf<T>::type fu_load(__amdgpu_buffer_rsrc_t rs,
+                                                           unsigned voff, unsigned soff) {
+    if constexpr (sizeof(T) == 2) {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0);
+    } else {
+        typedef unsigned u2v __attribute__((ext_vector_type(2)));
+        const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+        return uint2{v.x, v.y};
+    }
+}
+// hi16: 0xffff0000 held in a VGPR (a literal operand would halve the issue rate)
+template <typename T>
+__device__ __forceinline__ void fu_unpack(typename RawOf<T>::type r, float& e, float& o,
+                                          unsigned hi16) {
+    if constexpr (std::is_same<T, __bf16>::value) {
+        e = __builtin_bit_cast(float, r << 16);
+        o = __builtin_bit_cast(float, r & hi16);
+    } else if constexpr (sizeof(T) == 2) {
+        e = (float)__builtin_bit_cast(T, (unsigned short)(r & 0xffffu));
+        o = (float)__builtin_bit_cast(T, (unsigned short)(r >> 16));
+    } else {
+        e = __builtin_bit_cast(float, r.x);
+        o = __builtin_bit_cast(float, r.y);
+    }
+}
+template <typename T>
+__device__ __forceinline__ void fu_store(float e, float o, __amdgpu_buffer_rsrc_t rs,
+                                         unsigned voff, unsigned soff) {
+    if constexpr (sizeof(T) == 2) {
+        typedef T t2v __attribute__((ext_vector_type(2)));
+        const t2v p = {(T)e, (T)o};
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, p), rs, voff, soff, 0);
+    } else {
+        typedef unsigned u2v __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(
+            u2v{__builtin_bit_cast(unsigned, e), __builtin_bit_cast(unsigned, o)}, rs, voff, soff, 0);
+    }
+}
+
+template <int N> using IC = std::integral_constant<int, N>;
+__host__ __device__ constexpr int fu_mod(int a, int m) { return ((a % m) + m) % m; }
+
+// MD 0: rect -> hex -> HexConv2d -> hex -> rect (the pipeline).  MD 1: HexConv2d alone
+// (radius 2, stride 1, padding 1, pad value 0; HexFrames.py:96-169): the "u rows" are
+// the input hex rows themselves and conv rows are stored as they complete.
+template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD = 0>
+__global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(MD == 1 ? FU_WPE_CONV : FU_WPE)))
+void k_fused(const Tin* __restrict__ x,
+                                                      const float* __restrict__ kern,
+                                                      const float* __restrict__ bias,
+                                                      Tout* __restrict__ y, FusedGeom F) {
+    constexpr int CG = C / G, OG = O / G;
+    constexpr int PD = FU_PD;
+    static_assert(PD >= 1 && PD <= 4, "raw ring holds PD + 1 <= 6 rows");
+    using Raw = typename RawOf<Tin>::type;
+
+    // The 4 waves of a workgroup take 4 adjacent windows of one (image, band): a group
+    // of FU_GRP owned columns.  With STAGE, output rows go through LDS and the group
+    // stores them as aligned 128-B lines (a window's 240 owned bytes are not line
+    // aligned; partial-line stores cost ~20 % of HBM throughput, tools/microbench/walk2).
+    constexpr bool STAGE = FU_STAGE && sizeof(Tout) == 2;
+    constexpr int GW = FU_THREADS / 64;             // windows per group
+    constexpr int GDW = GW * FU_OWN / 2;            // dwords of one output row of a group
+    // per-wave u-row table {a, b, c, -}: u[r] = a*x[r-1] + b*x[r] + c*x[r+1]
+    __shared__ float4 lut_all[GW][FU_LUT];
+    __shared__ unsigned stg[STAGE ? 2 : 1][STAGE ? 6 : 1][STAGE ? O : 1][STAGE ? GDW + 4 : 1];
+    const int lane = threadIdx.x & 63;
+    const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float4* lut = lut_all[wslot];
+    const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
+    const int ngrp = (F.nwin + GW - 1) / GW;
+    const int grp = (int)(blk % ngrp);
+    const int64_t rest = blk / ngrp;
+    const int band = (int)(rest % F.nband);
+    const int64_t b = rest / F.nband;
+    if (b >= F.B) return;                         // uniform per workgroup
+    const int win = grp * GW + wslot;             // may be >= nwin: runs, owns nothing
+    const int W0 = win * FU_OWN - FU_HL;
+    const int ce = W0 + 2 * lane;                 // this lane's even column; odd = ce + 1
+    const int s0 = band * FU_RB;                  // first output row of the band
+    const int s1 = min(s0 + FU_RB, F.h2);
+
+    // ---- row table (fp64 lattice math, geometry_np.py:440-486) -------------
+    for (int e = lane; e < FU_LUT; e += 64) {
+        const int r = s0 - 1 + e;                 // u row
+        float4 t = {0.f, 0.f, 0.f, 0.f};
+        if (MD == 1) {
+            t.y = (r >= 0 && r < F.h) ? 1.f : 0.f;    // u row r = input row r; 0: padding row
+        } else if (r >= 0 && r < F.h1) {
+            const double i_ = axis_at(F.rxs, r) + (double)(F.h - 1) * 0.5;   // :440
+            const int in = (int)i_;                                          // :444
+            const double f = i_ - (double)(float)in;                         // :448
+            const float w0 = (in >= 0 && in < F.h) ? (float)(1.0 - f) : 0.f;
+            const float w1 = (in + 1 >= 0 && in + 1 < F.h) ? (float)f : 0.f;
+            if (in == r - 1) { t.x = w0; t.y = w1; }
+            else if (in == r) { t.y = w0; t.z = w1; }
+        }
+        lut[e] = t;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): own-wave LDS writes
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- per-lane column weights --------------------------------------------
+    // r2h (geometry_np.py:441-449, 514-517): u[q] = sum_k wr_k[q] v[q+k], k = -1..1
+    float we[3] = {0.f, 0.f, 0.f}, wo_[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2 && MD == 0; ++s) {
+        const int q = ce + s;
+        float* wr = s ? wo_ : we;
+        if (q >= 0 && q < F.w1) {
+            const double j_ = axis_at(F.rys, q) + (double)(F.w - 1) * 0.5;   // :441
+            const int jn = (int)j_;
+            const double jf = j_ - (double)(float)jn;
+#pragma unroll
+            for (int k = -1; k <= 1; ++k) {
+                const bool in_w = q + k >= 0 && q + k < F.w;
+                if (k == jn - q && in_w) wr[k + 1] += (float)(1.0 - jf);
+                if (k == jn + 1 - q && in_w) wr[k + 1] += (float)jf;
+            }
+        }
+    }
+    // h2r neighbour weights with the raster edge folded in (outside -> 0, :303-323)
+    // (w2 is even, so for an owned lane z[ce+1] and z[ce] are always inside: those two
+    // weights are the constant 0.25; only the outer neighbours can fall off the raster)
+    const float wn_o = (ce + 2 < F.w2) ? 0.25f : 0.f;   // even row, z[b+1], b = ce+1
+    const float wp_e = (ce - 1 >= 0) ? 0.25f : 0.f;     // odd row,  z[b-1], b = ce
+    const bool colin = ce >= 0 && ce < F.w;           // MD 1: input columns inside (w even)
+    const bool own = lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2 && ce >= 0 && ce < F.w2 &&
+                     win < F.nwin;
+    // staging slot of this lane's two output columns (non-owned lanes write a pad dword)
+    const int sidx = (lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2)
+                         ? wslot * (FU_OWN / 2) + lane - FU_HL / 2 : GDW + (lane & 3);
+
+    // ---- buffers: one descriptor per image, planes by per-lane offsets ---------
+    const int64_t cstride = (int64_t)F.h * F.w, ostride = (int64_t)F.h2 * F.w2;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + b * C * cstride), (short)0, (int)(C * cstride * (int64_t)sizeof(Tin)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(y + b * O * ostride), (short)0, (int)(O * ostride * (int64_t)sizeof(Tout)), 0x00020000);
+    const int lc = min(max(ce, 0), F.w - 2);            // clamped even load column
+    // one VGPR offset per lane; the plane of a channel is an SGPR offset
+    const unsigned xoff = (unsigned)lc * (unsigned)sizeof(Tin);
+    const unsigned yoff = own ? (unsigned)ce * (unsigned)sizeof(Tout) : 0x80000000u;
+    const unsigned xplane = (unsigned)(cstride * (int64_t)sizeof(Tin));
+    const unsigned yplane = (unsigned)(ostride * (int64_t)sizeof(Tout));
+    const unsigned xrow = (unsigned)F.w * (unsigned)sizeof(Tin);
+    const unsigned yrow = (unsigned)F.w2 * (unsigned)sizeof(Tout);
+    auto row_off = [&](int k) -> unsigned {             // clamped rect row (SALU)
+        if (FU_NOMEM) return 0u;
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(k, 0), F.h - 1) * xrow));
+    };
+
+    // ---- weights and bias in VGPRs -------------------------------------------------
+    // A VALU instruction with an SGPR (or literal) operand issues at half rate on gfx950
+    // (4.2 vs 2.3 cycles per wave-instruction, tools/microbench/issue.hip), so every
+    // FMA operand is a VGPR: an opaque per-lane zero offset makes these vector loads.
+    int vz = 0;
+    asm volatile("" : "+v"(vz));
+    float wk[O * CG * 7];
+#pragma unroll
+    for (int i = 0; i < O * CG * 7; ++i) wk[i] = kern[i + (FU_WSGPR ? 0 : vz)];
+    float bv[O];
+#pragma unroll
+    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] : 0.f;
+    float c75 = 0.75f, c25 = 0.25f;     // h2r weights as VGPR operands, not literals
+    asm volatile("" : "+v"(c75), "+v"(c25));
+    unsigned hi16 = 0xffff0000u;
+    asm volatile("" : "+v"(hi16));
+
+    // Column classes of the r2h horizontal taps over this wave's lanes (uniform): CD 1 if
+    // every live tap is at q-1 or q, CD 2 if at q or q+1 (one DPP shift and 2 FMAs per
+    // column instead of 2 and 3), CD 0 otherwise.  Same-size round trips have one
+    // window of class 0 per image row (where jn - q steps from -1 to 0).
+    const bool any_l = __builtin_amdgcn_ballot_w64(we[0] != 0.f || wo_[0] != 0.f) != 0;
+    const bool any_r = __builtin_amdgcn_ballot_w64(we[2] != 0.f || wo_[2] != 0.f) != 0;
+    const int cd = !FU_CD ? 0 : (!any_r ? 1 : (!any_l ? 2 : 0));
+
+    auto run = [&](auto CDc) {
+        constexpr int CD = decltype(CDc)::value;
+        // ---- state -----------------------------------------------------------------
+        Raw raw[6][C];                      // rect rows in flight, slot (row - s0) % 6
+        float XE[3][C], XO[3][C];           // rect rows as f32, slot (row - s0) % 3
+        float ZE[3][O], ZO[3][O];           // conv rows being accumulated, slot (row - s0) % 3
+
+        auto issue = [&](auto SLc, int k) {
+            constexpr int SL = decltype(SLc)::value;
+            const unsigned so = row_off(k);
+    #pragma unroll
+            for (int c = 0; c < C; ++c) raw[SL][c] = fu_load<Tin>(xrs, xoff, so + c * xplane);
+        };
+        auto convert = [&](auto RSc, auto XSc) {
+            constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
+    #pragma unroll
+            for (int c = 0; c < C; ++c) fu_unpack<Tin>(raw[RS][c], XE[XS][c], XO[XS][c], hi16);
+        };
+
+        // u row r (= s0 + PH + 1) from rect rows r-1, r, r+1 (ring slots PH, PH+1, PH+2
+        // mod 3) with table entry L, scattered into conv rows r+1 (above role; slot
+        // PH+2, started with the bias), r (centre; slot PH+1) and r-1 (below; slot PH).
+        auto urow = [&](auto PHc, float4 L, auto CENc, auto BELc) {
+            constexpr int PH = decltype(PHc)::value;
+            constexpr bool CEN = decltype(CENc)::value, BEL = decltype(BELc)::value;
+            constexpr int S0 = fu_mod(PH, 3), S1 = fu_mod(PH + 1, 3), S2 = fu_mod(PH + 2, 3);
+            constexpr int PB = fu_mod(PH, 2);       // parity of conv row r-1 (and r+1)
+            constexpr int PC = 1 - PB;              // parity of conv row r
+            float ue[C], uo[C];
+            if constexpr (MD == 1) {                // u = input row, 0 outside (padding 1, value 0)
+                const bool in_ = colin && L.y != 0.f;
+    #pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    ue[c] = in_ ? XE[S1][c] : 0.f;
+                    uo[c] = in_ ? XO[S1][c] : 0.f;
+                }
+            } else
+    #pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const float ve = fmaf(L.z, XE[S2][c], fmaf(L.y, XE[S1][c], L.x * XE[S0][c]));
+                const float vo = fmaf(L.z, XO[S2][c], fmaf(L.y, XO[S1][c], L.x * XO[S0][c]));
+                if constexpr (CD == 1) {            // taps q-1, q
+                    ue[c] = fmaf(we[1], ve, we[0] * f_prev(vo));
+                    uo[c] = fmaf(wo_[1], vo, wo_[0] * ve);
+                } else if constexpr (CD == 2) {     // taps q, q+1
+                    ue[c] = fmaf(we[2], vo, we[1] * ve);
+                    uo[c] = fmaf(wo_[2], f_next(ve), wo_[1] * vo);
+                } else {
+                    const float vpo = f_prev(vo), vne = f_next(ve);
+                    ue[c] = fmaf(we[2], vo, fmaf(we[1], ve, we[0] * vpo));
+                    uo[c] = fmaf(wo_[2], vne, fmaf(wo_[1], vo, wo_[0] * ve));
+                }
+            }
+    #pragma unroll
+            for (int c = 0; c < C; ++c) {
+                // u at column offsets -1 .. 2 of each of the lane's two columns
+                const float pe = f_prev(uo[c]);     // even col - 1
+                const float ne = f_next(ue[c]);     // odd col + 1 (= even col + 2)
+                const float no = OP == 0 ? f_next(uo[c]) : 0.f;   // odd col + 2
+                auto at_e = [&](int s) { return s == -1 ? pe : (s == 0 ? ue[c] : (s == 1 ? uo[c] : ne)); };
+                auto at_o = [&](int s) { return s == -1 ? ue[c] : (s == 0 ? uo[c] : (s == 1 ? ne : no)); };
+                const int g = c / CG, ci = c % CG;
+    #pragma unroll
+                for (int oo = 0; oo < OG; ++oo) {
+                    const int o = g * OG + oo;
+                    const float* w = &wk[(o * CG + ci) * 7];
+                    // above role (taps with ii == 0) of conv row r+1, parity PB
+    #pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int s = fu_tap_shift(t, PB, OP);
+                        if (ci == 0 && t == 0) {
+                            ZE[S2][o] = fmaf(w[t], at_e(s), bv[o]);
+                            ZO[S2][o] = fmaf(w[t], at_o(s), bv[o]);
+                        } else {
+                            ZE[S2][o] = fmaf(w[t], at_e(s), ZE[S2][o]);
+                            ZO[S2][o] = fmaf(w[t], at_o(s), ZO[S2][o]);
+                        }
+                    }
+                    if constexpr (CEN) {
+    #pragma unroll
+                        for (int t = 2; t < 5; ++t) {
+                            const int s = fu_tap_shift(t, PC, OP);
+                            ZE[S1][o] = fmaf(w[t], at_e(s), ZE[S1][o]);
+                            ZO[S1][o] = fmaf(w[t], at_o(s), ZO[S1][o]);
+                        }
+                    }
+                    if constexpr (BEL) {
+    #pragma unroll
+                        for (int t = 5; t < 7; ++t) {
+                            const int s = fu_tap_shift(t, PB, OP);
+                            ZE[S0][o] = fmaf(w[t], at_e(s), ZE[S0][o]);
+                            ZO[S0][o] = fmaf(w[t], at_o(s), ZO[S0][o]);
+                        }
+                    }
+                }
+            }
+        };
+
+        // conv row a2 (slot PH % 3, parity PH % 2) -> output row a2 (exact same-size h2r)
+        auto out_row = [&](auto PHc, auto SBc, int a2) {
+            constexpr int PH = decltype(PHc)::value;
+            constexpr int SB = STAGE ? decltype(SBc)::value : 0;
+            constexpr int S0 = PH % 3;
+            const unsigned so = FU_NOMEM ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
+    #pragma unroll
+            for (int o = 0; o < O; ++o) {
+                const float ze = ZE[S0][o], zo = ZO[S0][o];
+                float oe, oo;
+                if constexpr (MD == 1) {            // HexConv2d output row as is
+                    oe = ze;
+                    oo = zo;
+                } else if constexpr ((PH & 1) == 0) {      // 0.75 z[b] + 0.25 z[b+1]
+                    oe = fmaf(c25, zo, c75 * ze);
+                    oo = fmaf(wn_o, f_next(ze), c75 * zo);
+                } else {                            // 0.25 z[b-1] + 0.75 z[b]
+                    oe = fmaf(wp_e, f_prev(zo), c75 * ze);
+                    oo = fmaf(c25, ze, c75 * zo);
+                }
+                    if constexpr (STAGE) {
+                    typedef Tout t2v __attribute__((ext_vector_type(2)));
+                    const t2v pk = {(Tout)oe, (Tout)oo};
+                    stg[SB][PH][o][sidx] = __builtin_bit_cast(unsigned, pk);
+                } else {
+                    fu_store<Tout>(oe, oo, yrs, yoff, so + o * yplane);
+                }
+            }
+        };
+
+        // Store rows base .. base+nr-1 of the group from staging buffer SB: per (row, o) the
+        // group's segment of GDW dwords, as 4 line-aligned 256-B pieces (one dword per lane;
+        // lanes outside the segment store past the buffer range).  Rows are spread over
+        // the group's waves.
+        const int gcol0 = grp * GW * FU_OWN;                          // first column of the group
+        const int gdw = max(0, min(GDW, (F.w2 - gcol0) / 2));         // valid dwords per row
+        auto flush = [&](auto SBc, int base, int nr) {
+            constexpr int SB = decltype(SBc)::value;
+            __builtin_amdgcn_s_waitcnt(0xc07f);                       // lgkmcnt(0): our writes
+            __builtin_amdgcn_s_barrier();
+            // fixed trip count (the wait counts of the following steps stay exact): pairs
+            // past nr * O store nothing
+    #pragma unroll
+            for (int i = 0; i < (6 * O + GW - 1) / GW; ++i) {
+                const int p = wslot + GW * i;
+                const bool pv = p < nr * O;
+                const int row = pv ? p / O : 0, o = pv ? p - row * O : 0;
+                const unsigned S = (unsigned)((((int64_t)o * F.h2 + base + row) * F.w2 + gcol0) *
+                                              (int64_t)sizeof(Tout));
+                const unsigned A = S & ~127u;
+    #pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const unsigned gb = A + 256u * k + 4u * lane;
+                    const int d = (int)(gb - S) / 4;
+                    const bool ok = pv && gb >= S && d < gdw;
+                    const unsigned v = stg[SB][row][o][ok ? d : 0];
+                    __builtin_amdgcn_raw_buffer_store_b32(v, yrs, ok ? gb : 0x80000000u, 0, 0);
+                }
+            }
+        };
+
+        // ---- prologue: u rows s0-1 and s0 -------------------------------------------
+        {
+            Raw t0[C], t1[C], t2[C];
+            const unsigned o0 = row_off(s0 - 2), o1 = row_off(s0 - 1), o2 = row_off(s0);
+    #pragma unroll
+            for (int c = 0; c < C; ++c) {
+                t0[c] = fu_load<Tin>(xrs, xoff, o0 + c * xplane);
+                t1[c] = fu_load<Tin>(xrs, xoff, o1 + c * xplane);
+                t2[c] = fu_load<Tin>(xrs, xoff, o2 + c * xplane);
+            }
+            issue(IC<1>{}, s0 + 1);
+    #pragma unroll
+            for (int i = 0; i < PD; ++i) {          // ring: rect rows s0+2 .. s0+1+PD
+                if (i == 0) issue(IC<2>{}, s0 + 2);
+                if (i == 1) issue(IC<3>{}, s0 + 3);
+                if (i == 2) issue(IC<4>{}, s0 + 4);
+                if (i == 3) issue(IC<5>{}, s0 + 5);
+            }
+    #pragma unroll
+            for (int c = 0; c < C; ++c) {
+                fu_unpack<Tin>(t0[c], XE[1][c], XO[1][c], hi16);   // row s0-2 -> slot 1
+                fu_unpack<Tin>(t1[c], XE[2][c], XO[2][c], hi16);   // row s0-1 -> slot 2
+                fu_unpack<Tin>(t2[c], XE[0][c], XO[0][c], hi16);   // row s0   -> slot 0
+            }
+        }
+        urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});   // u row s0-1: above only
+        convert(IC<1>{}, IC<1>{});                                      // row s0+1 -> slot 1
+        urow(IC<-1>{}, lut[1], std::true_type{}, std::false_type{});    // u row s0: above, centre
+        // Drain the prologue's loads: the compiler's wait counts at the loop header merge the
+        // entry path with the back edge, and a ring load issued late on the entry path would
+        // otherwise put a near-zero vmcnt wait into every iteration.
+        if (FU_DRAIN) __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+
+        // ---- main loop ---------------------------------------------------------------
+        float4 lnext = lut[2];
+        auto step = [&](auto PHc, auto SBc, int a2) {
+            constexpr int PH = decltype(PHc)::value;
+            // keep each step's instructions inside the step: across a 12-step body the
+            // scheduler otherwise hoists loads many steps ahead (266 VGPRs, 1 wave / SIMD)
+            if (FU_SCHED) __builtin_amdgcn_sched_barrier(0);
+            convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row a2+2
+            issue(IC<(PH + 2 + PD) % 6>{}, a2 + 2 + PD);
+            const float4 L = lnext;
+            lnext = lut[min(a2 - s0 + 3, FU_LUT - 1)];
+            urow(PHc, L, std::true_type{}, std::true_type{});           // u row a2+1
+            out_row(PHc, SBc, a2);
+        };
+        // Full blocks of six unconditional steps: an exit or a conditional store between
+        // steps would let the compiler sink each rect-row load (and the last FMAs of a conv
+        // row) into the rarer block that consumes them, which removes the prefetch distance
+        // and serialises the accumulation.  The band's last h2 % 6 rows run as a tail.
+        // Two iterations per trip so the staging buffer index is a constant.
+        auto block6 = [&](auto SBc, int base) {
+            step(IC<0>{}, SBc, base);
+            step(IC<1>{}, SBc, base + 1);
+            step(IC<2>{}, SBc, base + 2);
+            step(IC<3>{}, SBc, base + 3);
+            step(IC<4>{}, SBc, base + 4);
+            step(IC<5>{}, SBc, base + 5);
+            if constexpr (STAGE) flush(SBc, base, 6);
+        };
+        auto tail = [&](auto SBc, int base) {
+            if (base >= s1) return;
+            step(IC<0>{}, SBc, base);
+            if (base + 1 < s1) {
+                step(IC<1>{}, SBc, base + 1);
+                if (base + 2 < s1) {
+                    step(IC<2>{}, SBc, base + 2);
+                    if (base + 3 < s1) {
+                        step(IC<3>{}, SBc, base + 3);
+                        if (base + 4 < s1) step(IC<4>{}, SBc, base + 4);
+                    }
+                }
+            }
+            if constexpr (STAGE) flush(SBc, base, s1 - base);
+        };
+        int base = s0;
+        if constexpr (STAGE || FU_L12) {   // two blocks per trip (constant staging index)
+            for (; base + 12 <= s1; base += 12) {
+                block6(IC<0>{}, base);
+                block6(IC<1>{}, base + 6);
+            }
+        } else {
+            for (; base + 12 <= s1; base += 6) block6(IC<0>{}, base);
+        }
+        if (base + 6 <= s1) {
+            block6(IC<0>{}, base);
+            tail(IC<1>{}, base + 6);
+        } else {
+            tail(IC<0>{}, base);
+        }
+    };
+    if constexpr (MD == 1) {
+        (void)cd;
+        run(IC<0>{});
+    } else {
+        if (FU_CD && cd == 1) run(IC<1>{});
+        else if (FU_CD && cd == 2) run(IC<2>{});
+        else run(IC<0>{});
+    }
+}
+
+}  // namespace hg
