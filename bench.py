@@ -10,9 +10,12 @@ gfx950 kernels of libhygrid_hip.so, with bf16 tensors between stages.
 
 Multi-GPU: one process per GPU (torchrun); every rank owns its own 128 images
 (weak scaling, no data-path collective).  value = all ranks' input pixels / the
-max-over-ranks wall time of K steps.  After the timed region, per-image
-checksums are all-gathered over RCCL, and (N>1) the full-output gather to rank 0
-is timed and reported on its own (`gather`), never folded into `value`.
+max-over-ranks wall time of K steps.  Every timed step ends with per-image,
+per-channel sums of a row sample of its output (every 64th row), all-gathered over
+RCCL at N > 1 (the collective stays inside the timed loop; a few KB per
+rank).  After the timed region, full per-image checksums are all-gathered, and
+(N>1) the full-output gather to rank 0 is timed and reported on its own
+(`gather`), never folded into `value`.
 
 Extra JSON fields: `kernels` (per-stage HIP-event times and algorithmic GB/s),
 `roofline` (dominant kernel vs 8 TB/s HBM), `cpu_baseline` (the C/OpenMP oracle
@@ -51,7 +54,8 @@ def parse():
     ap.add_argument("--channels", type=int, default=3)
     ap.add_argument("--cpu-images", type=int, default=64,
                     help="max images in the CPU-baseline sample (~10 s; 0 disables it)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu_count)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every CPU this process may run on (sched_getaffinity)")
     ap.add_argument("--no-gather", action="store_true", help="skip the timed output gather")
     ap.add_argument("--unfused", action="store_true",
                     help="time the three operators (r2h, HexConv2d, h2r) instead of the fused kernel")
@@ -59,19 +63,34 @@ def parse():
                     help="skip the secondary (unfused) measurement in the fused run")
     ap.add_argument("--no-pyramid", action="store_true",
                     help="skip the secondary config-5 line (8K fp16 3-level hex pyramid)")
+    ap.add_argument("--no-roundtrip", action="store_true",
+                    help="skip the secondary config-2 line (1080p fp32 rect->hex->rect)")
     ap.add_argument("--pyramid-batch", type=int, default=8, help="8K images per GPU (config 5)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-kernel HBM bytes from rocprofv3 PMC passes (optional)")
     return ap.parse_args()
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, kernel, bias):
     """Oracle (C/OpenMP fp64 restatement) on a bounded sample of the same workload:
-    whole images, one at a time, until ~10 s of CPU work (at most --cpu-images)."""
+    whole images, one at a time, until ~10 s of CPU work (at most --cpu-images), on
+    every CPU this process may run on."""
     import numpy as np
 
     from oracle import oracle as O
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = args.cpu_threads or avail or 1
     O.set_num_threads(threads)
     rng = np.random.default_rng(2)
     x = rng.random((1, args.channels, args.height, args.width))
@@ -86,7 +105,12 @@ def cpu_baseline(args, kernel, bias):
     return {"value": round(n * args.height * args.width / dt / 1e6, 3), "unit": "Mpix/s",
             "cores": threads, "kind": "port",
             "sample": f"{n} image(s) of {args.channels}x{args.height}x{args.width}, one at a "
-                      f"time (fp64 oracle/hg_oracle.c, r2h->HexConv2d->h2r), {dt:.2f} s"}
+                      f"time (fp64 oracle/hg_oracle.c, r2h->HexConv2d->h2r), {dt:.2f} s",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "cpus_available": avail,
+            "reference_measured": {"value": 1.05, "unit": "Mpix/s",
+                                   "what": "the reference's own geometry_np + HexFrames "
+                                           "(NumPy, one core), one 4K RGB image, survey "
+                                           "container (BASELINE.md section 2)"}}
 
 
 def main():
@@ -138,12 +162,28 @@ def main():
             ev.append(e)
         return y
 
-    def measure(fn, steps, warmup):
+    from HyGrid.dist import gather_sums
+    sums_buf = {}
+
+    def step_sums(y):
+        """Per-image, per-channel sums of every 64th output row, all-gathered over RCCL at
+        N > 1: the collective every timed step ends with (a few KB per rank)."""
+        s_ = y[:, :, ::64].float().sum((2, 3))
+        if world > 1:
+            key = tuple(s_.shape)
+            if key not in sums_buf:
+                sums_buf[key] = torch.empty((world * s_.shape[0],) + key[1:], dtype=s_.dtype,
+                                            device=s_.device)
+            gather_sums(s_, out=sums_buf[key])
+
+    def measure(fn, steps, warmup, collective=True):
         """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
         ev = []
         with torch.no_grad():
             for _ in range(warmup):
                 y = fn(False, ev)
+                if collective:
+                    step_sums(y)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -151,6 +191,8 @@ def main():
             t0 = time.perf_counter()
             for _ in range(steps):
                 y = fn(True, ev)
+                if collective:
+                    step_sums(y)
             torch.cuda.synchronize()
             if world > 1:
                 dist.barrier()
@@ -179,18 +221,26 @@ def main():
                for s in stages}
     dom = max(stages, key=lambda s: stage_ms[s])
     achieved = alg_bytes[dom] / (stage_ms[dom] * 1e-3) / 1e9
-    traffic = None
+    traffic, traffic_note = None, "no PMC profile"
     if os.path.exists(args.pmc_json):
         try:
+            from HyGrid._abi import kernel_source_digest
             with open(args.pmc_json) as f:
                 pmc = json.load(f)
-            if dom in pmc.get("kernels", {}):
+            here = kernel_source_digest()
+            if pmc.get("kernel_source_digest") != here:
+                # a profile of other kernel code is not evidence for this build
+                traffic_note = (f"{args.pmc_json} profiled kernel sources "
+                                f"{pmc.get('kernel_source_digest')}, this tree is {here}")
+            elif dom in pmc.get("kernels", {}):
                 traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"]
+                traffic_note = f"rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE, kernel sources {here}"
         except Exception as exc:  # keep the bench line even if the file is malformed
             log("pmc json unreadable:", exc)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "alg_bytes_per_launch": alg_bytes[dom],
+                "traffic": traffic, "traffic_source": traffic_note,
+                "alg_bytes_per_launch": alg_bytes[dom],
                 "limiter": "VALU issue for the fused kernel: a build whose loads/stores hit one "
                            "cache-resident row runs as fast (DESIGN.md section 9)"
                 if dom == "pipeline_r2h_conv_h2r" else "hbm"}
@@ -199,7 +249,7 @@ def main():
     if not args.unfused and not args.no_compare:
         # the three-operator chain on the same data, reported beside `value` (never as it)
         steps_u = max(2, args.steps // 2)
-        _, el_u, sms_u = measure(run_unfused, steps_u, 1)
+        _, el_u, sms_u = measure(run_unfused, steps_u, 1, collective=False)
         ks = ("rect_to_hex", "hexconv2d", "hex_to_rect")
         compare = {"path": "rect_to_hex -> HexConv2d -> hex_to_rect (3 kernels, bf16 between)",
                    "value": round(world * B * H * W * steps_u / el_u / 1e6, 1),
@@ -247,7 +297,7 @@ def main():
             return hx
 
         steps_p = max(2, args.steps // 2)
-        _, el_p, sms_p = measure(run_pyramid, steps_p, 1)
+        _, el_p, sms_p = measure(run_pyramid, steps_p, 1, collective=False)
         names = ["rect_to_hex"] + [f"{k}_l{lv}" for lv in range(3) for k in ("hexconv_dw", "hexresize")]
         pyramid = {"workload": "config5: 8K RGB fp16, r2h -> 3 x [depthwise Gaussian HexConv2d "
                                "-> hexresize /2]",
@@ -258,7 +308,7 @@ def main():
         del xp
 
     roundtrip = None
-    if not args.unfused and not args.no_pyramid:
+    if not args.unfused and not args.no_roundtrip:
         # BASELINE configs[1]: 1080p RGB fp32, batch 32 per GPU,
         # rect->hex bilinear -> hex->rect linear.  Reported beside `value`, never as it.
         Hr, Wr, Br = 1080, 1920, 32
@@ -278,7 +328,7 @@ def main():
             return out
 
         steps_r = max(2, args.steps // 2)
-        _, el_r, sms_r = measure(run_roundtrip, steps_r, 1)
+        _, el_r, sms_r = measure(run_roundtrip, steps_r, 1, collective=False)
         tb = Br * C * Hr * Wr * 4 * 2                 # each kernel: read once + write once
         roundtrip = {"workload": "config2: 1080p RGB fp32, rect->hex bilinear -> hex->rect linear",
                      "batch_per_gpu": Br, "dtype": "f32",

@@ -8,12 +8,31 @@ There is no CPU fallback: if the library or a HIP device is missing, the call
 raises.  (The CPU restatement under oracle/ is test infrastructure only.)
 """
 import ctypes
+import hashlib
 import os
 
 import torch  # noqa: F401  — load torch's HIP runtime before ours (shared SONAME)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HYGRID_LIB", os.path.join(_HERE, "_lib", "libhygrid_hip.so"))
+
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+
+def kernel_source_digest():
+    """sha256 (16 hex digits) over the kernel sources (csrc/*.hip, *.h, the C-ABI header):
+    the stamp that ties a profile (profiles/*/pmc_traffic.json) to the code it measured,
+    also where no git metadata travels (the GPU box gets a bare snapshot)."""
+    h = hashlib.sha256()
+    inc = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "hygrid.h")
+    files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                   if f.endswith((".hip", ".h", "Makefile")))
+    for f in files + ([inc] if os.path.exists(inc) else []):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
 
 # dtype codes (enum hg_dtype)
 HG_U8, HG_I8, HG_U16, HG_I16, HG_I32, HG_I64, HG_F16, HG_BF16, HG_F32, HG_F64 = range(10)

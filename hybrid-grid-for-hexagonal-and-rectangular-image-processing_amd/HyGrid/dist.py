@@ -10,7 +10,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["shard_range", "local_shard", "gather_to_root", "gather_checksums",
-           "image_checksums"]
+           "gather_sums", "image_checksums"]
 
 
 def shard_range(total, rank, world):
@@ -52,16 +52,37 @@ def gather_checksums(local, group=None):
     return torch.cat([o[: int(s.item())] for o, s in zip(out, sizes)])
 
 
-def gather_to_root(local, root=0, group=None):
+def gather_to_root(local, root=0, group=None, out=None):
     """Gather equal-shaped shards to `root` (P2P sends into root: xGMI ingress bound).
 
-    Returns the concatenated (world*B_local, ...) tensor on root, None elsewhere.
+    Root receives straight into one (world*B_local, ...) tensor (`out`, or a new one):
+    the shards land in its dim-0 slices, so root holds the result once, not the
+    per-rank buffers plus their concatenation.  Returns it on root, None elsewhere.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    local = local.contiguous()
     if rank == root:
-        bufs = [torch.empty_like(local) for _ in range(world)]
-        dist.gather(local.contiguous(), gather_list=bufs, dst=root, group=group)
-        return torch.cat(bufs)
-    dist.gather(local.contiguous(), dst=root, group=group)
+        shape = (world * local.shape[0],) + tuple(local.shape[1:])
+        if out is None:
+            out = torch.empty(shape, dtype=local.dtype, device=local.device)
+        elif tuple(out.shape) != shape or out.dtype != local.dtype or not out.is_contiguous():
+            raise ValueError(f"gather_to_root: out must be a contiguous {shape} {local.dtype} tensor")
+        dist.gather(local, gather_list=list(out.chunk(world)), dst=root, group=group)
+        return out
+    dist.gather(local, dst=root, group=group)
     return None
+
+
+def gather_sums(local, out=None, group=None):
+    """All-gather equal-shaped per-image reductions (B_local, C) into (world*B_local, C).
+
+    The collective the weak-scaling bench keeps inside its timed loop: a few
+    KB per rank, so it prices the RCCL latency, not xGMI bandwidth.
+    """
+    world = dist.get_world_size(group)
+    if out is None:
+        out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                          device=local.device)
+    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    return out

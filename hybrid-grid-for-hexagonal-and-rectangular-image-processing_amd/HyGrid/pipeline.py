@@ -13,7 +13,7 @@ import torch
 from . import ops
 from .HexFrames import HexConv2d
 
-__all__ = ["rect_hex_conv_rect", "fusable"]
+__all__ = ["rect_hex_conv_rect", "fusable", "hex_pyramid"]
 
 
 def fusable(conv):
@@ -42,3 +42,28 @@ def rect_hex_conv_rect(x, conv, hex_size=None, rect_size=None, out_dtype=None, f
     h = ops.rect_to_hex(x, hex_size, out_dtype=torch.float32)
     c = conv(h)
     return ops.hex_to_rect(c, rect_size, out_dtype=out_dtype)
+
+
+def hex_pyramid(x, conv, levels=3, out_dtype=None):
+    """Hex Gaussian pyramid (BASELINE config 5): rect -> hex at full size
+    (geometry_np.py:358-519), then `levels` x [conv (a HexConv2d, HexFrames.py:96-169)
+    -> hexresize to (h//2, w//2) (geometry_np.py:520-681)].  Returns the list of level
+    images [(B, C, h/2, w/2), (B, C, h/4, w/4), ...], each stored in out_dtype (default:
+    x's dtype when 16-bit, else fp32), as the operator chain stores them.
+    """
+    if out_dtype is None:
+        out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
+    H, W = x.shape[-2:]
+    hx = ops.rect_to_hex(x, (H, W), out_dtype=out_dtype)
+    prev = getattr(conv, "out_dtype", None)
+    conv.out_dtype = out_dtype
+    try:
+        outs = []
+        h_, w_ = H, W
+        for _ in range(levels):
+            h_, w_ = h_ // 2, w_ // 2
+            hx = ops.hexresize(conv(hx), (h_, w_), out_dtype=out_dtype)
+            outs.append(hx)
+    finally:
+        conv.out_dtype = prev
+    return outs

@@ -132,7 +132,10 @@ __host__ __device__ constexpr int fu_mod(int a, int m) { return ((a % m) + m) % 
 // (radius 2, stride 1, padding 1, pad value 0; HexFrames.py:96-169): the "u rows" are
 // the input hex rows themselves and conv rows are stored as they complete.
 template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD = 0>
-__global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(MD == 1 ? FU_WPE_CONV : FU_WPE)))
+// MD 1 with 16-bit input and output fits 128 VGPRs (4 waves per SIMD); an fp32 raw ring or
+// fp32 stores need more, and capping those at 128 spills to scratch inside the row loop.
+__global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(
+    (MD == 1 && sizeof(Tin) == 2 && sizeof(Tout) == 2) ? FU_WPE_CONV : FU_WPE)))
 void k_fused(const Tin* __restrict__ x,
                                                       const float* __restrict__ kern,
                                                       const float* __restrict__ bias,

@@ -276,6 +276,80 @@ void or_hexresize(const double* src, double* dst, int64_t planes, int64_t h, int
 }
 
 /* ---------------------------------------------------------------------------
+ * Adjoints of the three resamplers (the reference gets them from torch autograd
+ * through the indexing of geometry_torch.py:322-325; geometry_np.py:514-517 and
+ * :347-354 give the weights): gx = R^T gy.  Every output sample scatters its
+ * gradient onto the taps it read, with the forward's fp64 weights (bilinear:
+ * (1-fi)(1-fj), (1-fi)fj, fi(1-fj), fi*fj as products of the two blend stages;
+ * triangle: alpha, beta, gamma; nearest: 1 on the chosen tap).  Invalid taps
+ * (zero in the forward) receive nothing.  Planes are independent, so the plane
+ * loop is the parallel one and the scatter order inside a plane is sequential
+ * (deterministic).
+ * ------------------------------------------------------------------------- */
+static inline void add_tap(double* g, int64_t w, int64_t r, int64_t c, int valid, double v) {
+    if (valid) g[r * w + c] += v;
+}
+
+void or_rect_to_hex_backward(const double* gy, double* gx, int64_t planes, int64_t h, int64_t w,
+                             int64_t h1, int64_t w1, int interp) {
+#pragma omp parallel for schedule(static)
+    for (int64_t pl = 0; pl < planes; ++pl) {
+        double* g = gx + pl * h * w;
+        const double* gp = gy + pl * h1 * w1;
+        memset(g, 0, (size_t)(h * w) * sizeof(double));
+        for (int64_t a = 0; a < h1; ++a)
+            for (int64_t b = 0; b < w1; ++b) {
+                r2h_px p;
+                r2h_pixel(h, w, h1, w1, a, b, &p);
+                const int64_t i = p.i_n, j = p.j_n;
+                const double go = gp[a * w1 + b];
+                if (interp == 0) {                 /* :508-512: the chosen neighbour */
+                    const int k = p.argmin;
+                    add_tap(g, w, i + (k >> 1), j + (k & 1), (p.valid >> k) & 1, go);
+                } else {                           /* :514-517: out = fj*t2 + (1-fj)*t1 */
+                    const double gt1 = (1.0 - p.j_f) * go, gt2 = p.j_f * go;
+                    add_tap(g, w, i, j, p.valid & 1, (1.0 - p.i_f) * gt1);
+                    add_tap(g, w, i, j + 1, p.valid & 2, (1.0 - p.i_f) * gt2);
+                    add_tap(g, w, i + 1, j, p.valid & 4, p.i_f * gt1);
+                    add_tap(g, w, i + 1, j + 1, p.valid & 8, p.i_f * gt2);
+                }
+            }
+    }
+}
+
+static void tri_backward(const double* gy, double* gx, int64_t planes, int64_t h, int64_t w,
+                         int64_t h1, int64_t w1, int interp, double margin) {
+#pragma omp parallel for schedule(static)
+    for (int64_t pl = 0; pl < planes; ++pl) {
+        double* g = gx + pl * h * w;
+        const double* gp = gy + pl * h1 * w1;
+        memset(g, 0, (size_t)(h * w) * sizeof(double));
+        for (int64_t a = 0; a < h1; ++a)
+            for (int64_t b = 0; b < w1; ++b) {
+                tri_px p;
+                tri_pixel(h, w, h1, w1, a, b, margin, &p);
+                const double go = gp[a * w1 + b];
+                if (interp == 0) {
+                    const int k = p.argmin;
+                    add_tap(g, w, p.r[k], p.c[k], p.vk[k], go);
+                } else {                           /* :354 */
+                    const double wt[3] = {p.alpha, p.beta, p.gamma};
+                    for (int k = 0; k < 3; ++k) add_tap(g, w, p.r[k], p.c[k], p.vk[k], wt[k] * go);
+                }
+            }
+    }
+}
+
+void or_hex_to_rect_backward(const double* gy, double* gx, int64_t planes, int64_t h, int64_t w,
+                             int64_t h1, int64_t w1, int interp) {
+    tri_backward(gy, gx, planes, h, w, h1, w1, interp, 0.75);
+}
+void or_hexresize_backward(const double* gy, double* gx, int64_t planes, int64_t h, int64_t w,
+                           int64_t h1, int64_t w1, int interp) {
+    tri_backward(gy, gx, planes, h, w, h1, w1, interp, 0.5);
+}
+
+/* ---------------------------------------------------------------------------
  * HexConv2d (HexFrames.py:22-185, heximage_to_type1 :417-445, pad :13-21)
  *
  * Restated without materialising the type1 image.  With P = pad(x, p), H' = H+2p,
@@ -320,11 +394,22 @@ static inline int64_t pad_index(int64_t i, int64_t n, int mode) {
     }
 }
 
+/* torch F.pad's rules for the non-constant modes (the reference pads with F.pad,
+ * HexFrames.py:13-21): reflect needs padding < size, circular padding <= size.  Outside
+ * them torch raises; the mirror loop of pad_index would not terminate. */
+static int pad_args_ok(int64_t h, int64_t w, int p, int mode) {
+    if (mode == OR_PAD_REFLECT && p > 0 && (p >= h || p >= w)) return 0;
+    if (mode != OR_PAD_CONSTANT && p > 0 && (h == 0 || w == 0)) return 0;
+    if (mode == OR_PAD_CIRCULAR && (p > h || p > w)) return 0;
+    return 1;
+}
+
 int or_hexconv2d(const double* x, const double* kern, const double* bias, double* y,
                  int64_t B, int64_t C, int64_t O, int64_t h, int64_t w, int r, int s, int p,
                  int d, int groups, int off, int pad_mode, double pad_value) {
     int64_t ho, wo;
     int st = or_hexconv2d_out_shape(h, w, r, s, p, d, &ho, &wo);
+    if (st == 0 && !pad_args_ok(h, w, p, pad_mode)) st = -2;
     if (st) return st;
     if (groups < 1 || C % groups || O % groups) return -1;
     int K = 3 * r * r - 3 * r + 1;                    /* :52 */
@@ -388,6 +473,7 @@ int or_hexconv2d_backward(const double* x, const double* kern, const double* gy,
                           int pad_mode, double pad_value) {
     int64_t ho, wo;
     int st = or_hexconv2d_out_shape(h, w, r, s, p, d, &ho, &wo);
+    if (st == 0 && !pad_args_ok(h, w, p, pad_mode)) st = -2;
     if (st) return st;
     if (groups < 1 || C % groups || O % groups) return -1;
     int K = 3 * r * r - 3 * r + 1;

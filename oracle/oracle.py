@@ -12,6 +12,9 @@ Each function mirrors one reference entry point (paths under /root/reference):
   hexresize     HyGrid/geometry_np.py:520-681
   hexconv2d     HyGrid/HexFrames.py:96-169
   hexconv2d_backward  the adjoint of hexconv2d (reference: torch autograd of :96-169)
+  rect_to_hex_backward / hex_to_rect_backward / hexresize_backward  the adjoints of the
+                three resamplers (reference: torch autograd through the indexing of
+                HyGrid/geometry_torch.py:322-325; weights geometry_np.py:514-517, :347-354)
   image_geometric_transformation  HyGrid/geometry_np.py:6-189 (NumPy restatement;
                 nearest per HyGrid/geometry_torch.py:165-173)
   hex_pool2d    HyGrid/HexFrames.py:286-343 windows, :461-479 reductions, and their
@@ -50,7 +53,9 @@ def lib():
         for name in ("or_r2h_maps", "or_h2r_maps", "or_hexresize_maps"):
             getattr(L, name).argtypes = [_i64] * 4 + [_ip, _dp]
             getattr(L, name).restype = None
-        for name in ("or_rect_to_hex", "or_hex_to_rect", "or_hexresize"):
+        for name in ("or_rect_to_hex", "or_hex_to_rect", "or_hexresize",
+                     "or_rect_to_hex_backward", "or_hex_to_rect_backward",
+                     "or_hexresize_backward"):
             getattr(L, name).argtypes = [_dp, _dp] + [_i64] * 5 + [ctypes.c_int]
             getattr(L, name).restype = None
         L.or_hexconv2d_out_shape.argtypes = [_i64, _i64] + [ctypes.c_int] * 4 + [
@@ -133,6 +138,28 @@ def hex_to_rect(x, size=None, interp=1):
 
 def hexresize(x, size, interp=1):
     return _resample(lib().or_hexresize, x, size, interp)
+
+
+def _resample_backward(fn, gy, size, interp):
+    """gx (planes, h, w) = R^T gy for a resample from (h, w) to gy's (h1, w1)."""
+    planes, lead = _as_planes(gy)
+    n, h1, w1 = planes.shape
+    h, w = size
+    out = np.empty((n, h, w), np.float64)
+    fn(_dptr(planes), _dptr(out), n, h, w, h1, w1, int(interp))
+    return out.reshape(tuple(lead) + (h, w))
+
+
+def rect_to_hex_backward(gy, src_size, interp=1):
+    return _resample_backward(lib().or_rect_to_hex_backward, gy, src_size, interp)
+
+
+def hex_to_rect_backward(gy, src_size, interp=1):
+    return _resample_backward(lib().or_hex_to_rect_backward, gy, src_size, interp)
+
+
+def hexresize_backward(gy, src_size, interp=1):
+    return _resample_backward(lib().or_hexresize_backward, gy, src_size, interp)
 
 
 def hexconv2d_out_shape(h, w, r, stride=1, padding=0, dilation=1):

@@ -98,3 +98,34 @@ def test_fused_conv_4k_batch_matches_stream_kernel():
     ref = _other_kernel(ops.hexconv2d, x, k, b, 0, 2, padding=1, out_dtype=torch.float32)
     scale = float(ref.abs().max())
     torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5 * scale)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("off", [0, 1])
+def test_fused_conv_nan_inf_positions_match_stream_kernel(dt, off):
+    """Non-finite inputs on the raster border, at the 120-column window edges and at the
+    126-row band edges: MD 1 builds its padding by selecting zeros (fused_kernel.h), so a
+    boundary row's or column's NaN must reach exactly the outputs whose taps read it,
+    as in the register-streaming kernel (HYGRID_FCONV=0)."""
+    B, C, h, w = 2, 3, 260, 372
+    k, b = _weights(3, 3, 17 + off)
+    g = torch.Generator(device=DEV).manual_seed(13)
+    x = torch.rand((B, C, h, w), generator=g, device=DEV)
+    nan, inf = float("nan"), float("inf")
+    x[0, 0, 0, :] = nan                   # first row
+    x[0, 1, h - 1, 5] = inf               # last row
+    x[0, 2, 40, 0] = -inf                 # first column
+    x[1, 0, 77, w - 1] = nan              # last column
+    for c0 in (119, 120, 239, 240, 359, 360):   # window edges (owned columns 0..119, ...)
+        x[1, 1, 30 + c0 % 7, c0] = nan
+    for r0 in (125, 126, 251, 252):       # band edges (126-row bands)
+        x[1, 2, r0, 61 + r0 % 5] = inf
+    x = x.to(dt)
+    y = ops.hexconv2d(x, k, b, off, 2, padding=1, out_dtype=torch.float32)
+    ref = _other_kernel(ops.hexconv2d, x, k, b, off, 2, padding=1, out_dtype=torch.float32)
+    assert torch.equal(torch.isnan(y), torch.isnan(ref))
+    assert torch.equal(torch.isinf(y), torch.isinf(ref))
+    assert torch.equal(torch.sign(y[torch.isinf(y)]), torch.sign(ref[torch.isinf(ref)]))
+    fin = torch.isfinite(ref)
+    scale = float(ref[fin].abs().max())
+    torch.testing.assert_close(y[fin], ref[fin], rtol=1e-5, atol=1e-5 * scale)

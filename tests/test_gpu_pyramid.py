@@ -1,0 +1,115 @@
+"""BASELINE config 5 as a chain: the 8K fp16 hex Gaussian pyramid the bench times
+(rect->hex bilinear at full size, then 3 x [depthwise HexConv2d(3,3,0,2,padding=1,
+groups=3) with taps [1,1,1,6,1,1,1]/12 -> hexresize to (h//2, w//2) linear]) against the
+fp64 oracle chain (geometry_np.py:358-519, HexFrames.py:96-169, geometry_np.py:520-681).
+
+Every stage stores fp16, so the oracle chain rounds to fp16 after each stage too (the
+same storage points); the remaining differences are one fp16 rounding per stored stage
+that the fp32 arithmetic of the kernels moves across a rounding boundary.  Tolerance:
+7 stored stages x half an fp16 ulp at the top of the range (2^-11), i.e.
+atol = 7 * 2^-11 * max|ref|; the unrounded fp64 chain is checked at 2^-8."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from HyGrid import ops  # noqa: E402
+from HyGrid.HexFrames import HexConv2d  # noqa: E402
+from HyGrid.pipeline import hex_pyramid  # noqa: E402
+
+DEV = torch.device("cuda:0")
+TAPS = [1, 1, 1, 6, 1, 1, 1]
+
+
+def gaussian_conv():
+    conv = HexConv2d(3, 3, 0, 2, padding=1, groups=3, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.kernel.copy_(torch.tensor(TAPS, dtype=torch.float32, device=DEV).div_(12)
+                          .expand_as(conv.kernel))
+    conv.out_dtype = torch.float16
+    return conv
+
+
+def gpu_chain(x, conv, levels=3):
+    """The bench's unfused pyramid (bench.py run_pyramid), level outputs returned."""
+    H, W = x.shape[-2:]
+    with torch.no_grad():
+        hx = ops.rect_to_hex(x, (H, W), out_dtype=torch.float16)
+        outs = []
+        h_, w_ = H, W
+        for _ in range(levels):
+            hx = conv(hx)
+            h_, w_ = h_ // 2, w_ // 2
+            hx = ops.hexresize(hx, (h_, w_), out_dtype=torch.float16)
+            outs.append(hx)
+    return outs
+
+
+def oracle_chain(x, kern, levels=3, f16=True):
+    rnd = (lambda a: a.astype(np.float16).astype(np.float64)) if f16 else (lambda a: a)
+    H, W = x.shape[-2:]
+    hx = rnd(O.rect_to_hex(x, (H, W), 1))
+    outs = []
+    h_, w_ = H, W
+    for _ in range(levels):
+        hx = rnd(O.hexconv2d(hx, kern, None, 0, 2, padding=1, groups=3))
+        h_, w_ = h_ // 2, w_ // 2
+        hx = rnd(O.hexresize(hx, (h_, w_), 1))
+        outs.append(hx)
+    return outs
+
+
+def check(outs, refs, atol_ulps):
+    for lv, (y, ref) in enumerate(zip(outs, refs)):
+        y = y.double().cpu().numpy().reshape(ref.shape)
+        scale = np.abs(ref).max()
+        err = np.abs(y - ref).max()
+        assert err <= atol_ulps * scale, f"level {lv}: max err {err:.3e} > {atol_ulps * scale:.3e}"
+
+
+@pytest.mark.parametrize("H,W", [(540, 960), (136, 250), (70, 90)])
+def test_pyramid_chain_vs_oracle(H, W):
+    conv = gaussian_conv()
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.rand((2, 3, H, W), generator=gen, device=DEV, dtype=torch.float16)
+    outs = gpu_chain(x, conv)
+    xd = x.double().cpu().numpy().reshape(-1, H, W)
+    kern = conv.kernel.detach().cpu().numpy()
+    check(outs, [r.reshape(o.shape) for r, o in zip(oracle_chain(xd, kern), outs)], 7 * 2 ** -11)
+    check(outs, [r.reshape(o.shape) for r, o in zip(oracle_chain(xd, kern, f16=False), outs)],
+          2 ** -8)
+
+
+def test_pyramid_8k_full_image_vs_oracle():
+    """One full 4320x7680 RGB image through all three levels (config 5's geometry)."""
+    conv = gaussian_conv()
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.rand((1, 3, 4320, 7680), generator=gen, device=DEV, dtype=torch.float16)
+    outs = gpu_chain(x, conv)
+    assert [tuple(o.shape) for o in outs] == [(1, 3, 2160, 3840), (1, 3, 1080, 1920),
+                                              (1, 3, 540, 960)]
+    xd = x.double().cpu().numpy().reshape(-1, 4320, 7680)
+    refs = oracle_chain(xd, conv.kernel.detach().cpu().numpy())
+    check(outs, [r.reshape(o.shape) for r, o in zip(refs, outs)], 7 * 2 ** -11)
+
+
+@pytest.mark.parametrize("H,W", [(540, 960), (136, 250)])
+def test_hex_pyramid_entry_matches_chain(H, W):
+    """HyGrid.pipeline.hex_pyramid (the bench's config-5 step) gives the operator chain's
+    levels bit for bit, or within one fp16 rounding per stage where it fuses stages."""
+    conv = gaussian_conv()
+    gen = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.rand((2, 3, H, W), generator=gen, device=DEV, dtype=torch.float16)
+    outs = gpu_chain(x, conv)
+    with torch.no_grad():
+        got = hex_pyramid(x, conv, levels=3)
+    for a, b in zip(got, outs):
+        assert a.shape == b.shape and a.dtype == b.dtype
+        scale = b.double().abs().max().item()
+        assert (a.double() - b.double()).abs().max().item() <= 7 * 2 ** -11 * scale

@@ -62,3 +62,40 @@ def test_grad_dtype_and_batch(dtype):
     x2 = x.detach()[:1].clone().requires_grad_(True)
     ops.hex_to_rect(ops.rect_to_hex(x2, (48, 80)), (48, 80)).float().sum().backward()
     torch.testing.assert_close(x.grad[:1].float(), x2.grad.float(), rtol=1e-5, atol=1e-5)
+
+
+ORACLE_BWD = {"r2h": "rect_to_hex_backward", "h2r": "hex_to_rect_backward",
+              "hexresize": "hexresize_backward"}
+
+
+def _grad_vs_oracle(op, shape, interp, dtype, planes=2, seed=3):
+    from oracle import oracle as O
+    h, w, h1, w1 = shape
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.rand((planes, h, w), generator=g, device=DEV, dtype=dtype, requires_grad=True)
+    y = FNS[op](x, (h1, w1), interp=interp)
+    gy = torch.randn(y.shape, generator=g, device=DEV, dtype=y.dtype)
+    y.backward(gy)
+    ref = getattr(O, ORACLE_BWD[op])(gy.double().cpu().numpy(), (h, w), interp)
+    return x.grad.double().cpu().numpy(), ref
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("op", ["r2h", "h2r", "hexresize"])
+@pytest.mark.parametrize("interp", [0, 1])
+def test_backward_elementwise_vs_oracle_adjoint(shape, op, interp):
+    """hg_resample_backward against the fp64 oracle transpose (oracle/hg_oracle.c
+    or_*_backward), element by element.  fp64 accumulation: the atomic scatter sums the
+    same <= 4 products in another order (rtol 1e-12); fp32: rtol 1e-5 of max|ref|."""
+    got, ref = _grad_vs_oracle(op, shape, interp, torch.float64)
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-12 * np.abs(ref).max())
+    got, ref = _grad_vs_oracle(op, shape, interp, torch.float32)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("op,shape", [("r2h", (2160, 3840, 2160, 3840)),
+                                      ("h2r", (2160, 3840, 2160, 3840)),
+                                      ("hexresize", (4320, 7680, 2160, 3840))])
+def test_backward_4k_plane_vs_oracle_adjoint(op, shape):
+    got, ref = _grad_vs_oracle(op, shape, 1, torch.float32, planes=1)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
