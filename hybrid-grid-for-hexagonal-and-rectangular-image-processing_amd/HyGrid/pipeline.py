@@ -13,7 +13,7 @@ import torch
 from . import ops
 from .HexFrames import HexConv2d
 
-__all__ = ["rect_hex_conv_rect", "fusable", "hex_pyramid"]
+__all__ = ["rect_hex_conv_rect", "fusable", "hex_pyramid", "pyramid_fusable"]
 
 
 def fusable(conv):
@@ -44,21 +44,55 @@ def rect_hex_conv_rect(x, conv, hex_size=None, rect_size=None, out_dtype=None, f
     return ops.hex_to_rect(c, rect_size, out_dtype=out_dtype)
 
 
-def hex_pyramid(x, conv, levels=3, out_dtype=None):
+def pyramid_fusable(conv):
+    """A depthwise (groups == C == O), radius-2, stride-1, dilation-1 HexConv2d padded
+    with constant 0 by one sample: what the fused pyramid level kernel implements."""
+    return (isinstance(conv, HexConv2d) and conv.hexkernel_radius == 2 and conv.stride == 1
+            and conv.dilation == 1 and conv.padding_mode in ("constant", "zeros")
+            and conv.pad == 1 and float(conv.padding_value) == 0.0
+            and conv.in_channels == conv.out_channels == conv.groups
+            and conv.kernel.dtype == torch.float32)
+
+
+def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=False):
     """Hex Gaussian pyramid (BASELINE config 5): rect -> hex at full size
     (geometry_np.py:358-519), then `levels` x [conv (a HexConv2d, HexFrames.py:96-169)
     -> hexresize to (h//2, w//2) (geometry_np.py:520-681)].  Returns the list of level
     images [(B, C, h/2, w/2), (B, C, h/4, w/4), ...], each stored in out_dtype (default:
-    x's dtype when 16-bit, else fp32), as the operator chain stores them.
+    x's dtype when 16-bit, else fp32).
+
+    With a depthwise radius-2 conv (pyramid_fusable) and no autograd, every level is one
+    pass of hg_hex_pyramid_level after a rect -> hex pass stored in out_dtype (the
+    row-streaming resampler; measured faster than folding rect -> hex into level 0,
+    l0_from_rect=True: 1.71 vs 2.37 ms on config 5, tools/ab_pyramid.py),
+    with the intermediates in fp32 on chip; otherwise the operator chain, which stores
+    every stage in out_dtype.
     """
     if out_dtype is None:
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
     H, W = x.shape[-2:]
+    outs = []
+    if fused and pyramid_fusable(conv) and not torch.is_grad_enabled():
+        cur, h_, w_, ok = x, H, W, True
+        if not l0_from_rect:
+            cur = ops.rect_to_hex(x, (H, W), out_dtype=out_dtype)
+        for lv in range(levels):
+            h_, w_ = h_ // 2, w_ // 2
+            y = ops.hex_pyramid_level(cur, conv.kernel, conv.bias, (h_, w_),
+                                      int(conv.even_odd_offset),
+                                      from_rect=(lv == 0 and l0_from_rect), out_dtype=out_dtype)
+            if y is None:
+                ok = False
+                break
+            outs.append(y)
+            cur = y
+        if ok:
+            return outs
+        outs = []
     hx = ops.rect_to_hex(x, (H, W), out_dtype=out_dtype)
     prev = getattr(conv, "out_dtype", None)
     conv.out_dtype = out_dtype
     try:
-        outs = []
         h_, w_ = H, W
         for _ in range(levels):
             h_, w_ = h_ // 2, w_ // 2

@@ -219,6 +219,23 @@ int hg_pipeline_r2h_conv_h2r(const void* x, const float* kernel, const float* bi
                              int64_t h2, int64_t w2, int padding, int groups,
                              int even_odd_offset, double pad_value, void* stream);
 
+/* One level of a hex Gaussian pyramid (BASELINE config 5) in one pass:
+ *   from_rect = 0:  y = hexresize(HexConv2d_dw(x), (h1, w1))
+ *   from_rect = 1:  y = hexresize(HexConv2d_dw(rect_to_hex(x, (h, w), 'bilinear')), (h1, w1))
+ * Replaces the chain rect_to_hex_resample (geometry_np.py:358-519) ->
+ * HexConv2d(C, C, even_odd_offset, 2, stride=1, padding=1, dilation=1, groups=C,
+ * padding_mode='constant', padding_value=0) (HexFrames.py:22-169) -> hexresize(.,
+ * (h1, w1), 'linear') (geometry_np.py:520-681).  x: (B, C, h, w); taps: (C, 7) float32
+ * (the depthwise kernel, HexConv2d.kernel (C, 1, 1, 7)); bias: (C,) float32 or NULL;
+ * y: (B, C, h1, w1).  Intermediates stay on chip in fp32.  x_dtype in {F16, BF16, F32},
+ * y_dtype in {x_dtype, F32} (F32 in: also F16, BF16).  Returns HG_EUNSUP when the
+ * resize footprint does not fit the kernel's tile (e.g. > 2x downsampling) or the r2h
+ * lattice is not near-identity (then run the operators instead). */
+int hg_hex_pyramid_level(const void* x, void* y, int x_dtype, int y_dtype, int64_t batch,
+                         int64_t channels, int64_t h, int64_t w, int64_t h1, int64_t w1,
+                         const float* taps, const float* bias, int even_odd_offset,
+                         int from_rect, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

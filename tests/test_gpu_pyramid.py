@@ -79,7 +79,7 @@ def test_pyramid_chain_vs_oracle(H, W):
     gen = torch.Generator(device=DEV).manual_seed(5)
     x = torch.rand((2, 3, H, W), generator=gen, device=DEV, dtype=torch.float16)
     outs = gpu_chain(x, conv)
-    xd = x.double().cpu().numpy().reshape(-1, H, W)
+    xd = x.double().cpu().numpy()
     kern = conv.kernel.detach().cpu().numpy()
     check(outs, [r.reshape(o.shape) for r, o in zip(oracle_chain(xd, kern), outs)], 7 * 2 ** -11)
     check(outs, [r.reshape(o.shape) for r, o in zip(oracle_chain(xd, kern, f16=False), outs)],
@@ -94,7 +94,7 @@ def test_pyramid_8k_full_image_vs_oracle():
     outs = gpu_chain(x, conv)
     assert [tuple(o.shape) for o in outs] == [(1, 3, 2160, 3840), (1, 3, 1080, 1920),
                                               (1, 3, 540, 960)]
-    xd = x.double().cpu().numpy().reshape(-1, 4320, 7680)
+    xd = x.double().cpu().numpy()
     refs = oracle_chain(xd, conv.kernel.detach().cpu().numpy())
     check(outs, [r.reshape(o.shape) for r, o in zip(refs, outs)], 7 * 2 ** -11)
 
@@ -113,3 +113,55 @@ def test_hex_pyramid_entry_matches_chain(H, W):
         assert a.shape == b.shape and a.dtype == b.dtype
         scale = b.double().abs().max().item()
         assert (a.double() - b.double()).abs().max().item() <= 7 * 2 ** -11 * scale
+
+
+LEVEL_CASES = [  # (B, C, h, w, h1, w1)
+    (2, 3, 64, 130, 32, 65), (1, 3, 37, 53, 18, 26), (1, 1, 200, 250, 100, 125),
+    (2, 3, 33, 500, 16, 250), (1, 3, 17, 9, 8, 4), (1, 2, 70, 90, 35, 45), (1, 3, 40, 70, 40, 70),
+]
+
+
+@pytest.mark.parametrize("case", LEVEL_CASES)
+@pytest.mark.parametrize("from_rect", [False, True])
+@pytest.mark.parametrize("off", [0, 1])
+def test_pyramid_level_fp32_vs_oracle(case, from_rect, off):
+    """hg_hex_pyramid_level (fp32 in/out) against the oracle chain at rtol 1e-5: ragged
+    tiles (16 x 62 outputs), odd sizes, upsampling-free sizes, 1-3 channels, with bias."""
+    B, C, h, w, h1, w1 = case
+    g = torch.Generator().manual_seed(h * 7 + w + off)
+    taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
+    bias = (torch.rand((C,), generator=g) - 0.5).to(DEV)
+    x = torch.rand((B, C, h, w), generator=g).to(DEV)
+    y = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=from_rect,
+                              out_dtype=torch.float32)
+    assert y is not None
+    xd = x.double().cpu().numpy()
+    hx = O.rect_to_hex(xd, (h, w), 1) if from_rect else xd
+    c = O.hexconv2d(hx, taps.cpu().double().numpy(), bias.cpu().double().numpy(), off, 2,
+                    padding=1, groups=C)
+    ref = O.hexresize(c, (h1, w1), 1)
+    got = y.double().cpu().numpy()
+    scale = max(np.abs(ref).max(), 1e-30)
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5 * scale)
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_pyramid_level_16bit_and_nan(dt):
+    """16-bit in/out within one output rounding of the fp64 chain; a NaN in the input
+    reaches exactly the outputs whose taps read it (as in the operator chain)."""
+    B, C, h, w = 1, 3, 96, 200
+    g = torch.Generator().manual_seed(3)
+    taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
+    x = torch.rand((B, C, h, w), generator=g).to(DEV).to(dt)
+    x[0, 1, 50, 100] = float("nan")
+    y = ops.hex_pyramid_level(x, taps, None, (h // 2, w // 2), 0, from_rect=False)
+    assert y is not None and y.dtype == dt
+    with torch.no_grad():
+        conv = HexConv2d(3, 3, 0, 2, padding=1, groups=3, bias=False).to(DEV)
+        conv.kernel.copy_(taps)
+        ref = ops.hexresize(conv(x.float()), (h // 2, w // 2), out_dtype=torch.float32)
+    assert torch.equal(torch.isnan(y), torch.isnan(ref))
+    fin = torch.isfinite(ref)
+    ulp = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
+    scale = float(ref[fin].abs().max())
+    torch.testing.assert_close(y.float()[fin], ref[fin], rtol=ulp, atol=ulp * scale)
