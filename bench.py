@@ -65,6 +65,8 @@ def parse():
                     help="skip the secondary config-5 line (8K fp16 3-level hex pyramid)")
     ap.add_argument("--no-roundtrip", action="store_true",
                     help="skip the secondary config-2 line (1080p fp32 rect->hex->rect)")
+    ap.add_argument("--no-wide-conv", action="store_true",
+                    help="skip the secondary wide-channel HexConv2d line (64->64, 1080p)")
     ap.add_argument("--pyramid-batch", type=int, default=8, help="8K images per GPU (config 5)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-kernel HBM bytes from rocprofv3 PMC passes (optional)")
@@ -374,6 +376,40 @@ def main():
                                  for k, m in zip(("rect_to_hex", "hex_to_rect"), sms_r)}}
         del xr
 
+    wide = None
+    if not args.unfused and not args.no_wide_conv:
+        # HexConvModule-sized HexConv2d (HexModules.py:97-288): 64 -> 64 channels on a
+        # 1080p bf16 batch of 4, the implicit GEMM on the f32 matrix cores (conv_mfma.hip).
+        # Compute-bound: reported in TFLOP/s (2 * O * 7 * C per output sample) against the
+        # f32 MFMA peak (157.3 TF, MI355X_MICROARCH.md).  Beside `value`, never as it.
+        Bw, Cw, Ow, Hw, Ww = 4, 64, 64, 1080, 1920
+        xw = (torch.rand((Bw, Cw, Hw, Ww), generator=gen, device=dev) - 0.5).to(bf16)
+        torch.manual_seed(5)
+        wconv = HexConv2d(Cw, Ow, 0, 2, padding=1, bias=True).to(dev)
+        wconv.out_dtype = bf16
+
+        def run_wide(record, ev):
+            if record:
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                e[0].record()
+            out = wconv(xw)
+            if record:
+                e[1].record()
+                ev.append(e)
+            return out
+
+        steps_w = max(2, args.steps // 2)
+        _, el_w, sms_w = measure(run_wide, steps_w, 1, collective=False)
+        flop = 2.0 * Ow * 7 * Cw * Bw * Hw * Ww
+        tf = flop / (sms_w[0] * 1e-3) / 1e12
+        wide = {"workload": f"HexConv2d({Cw},{Ow},0,2,padding=1) bf16, {Bw}x{Cw}x{Hw}x{Ww}",
+                "ms": round(sms_w[0], 4), "TFLOP_s": round(tf, 2),
+                "roofline": {"bound": "mfma", "peak": 157.3, "unit": "TFLOP/s",
+                             "frac": round(tf / 157.3, 4),
+                             "note": "f32 MFMA (exact fp32 products; 16-bit inputs staged "
+                                     "as f32)"}}
+        del xw
+
     # checksums over RCCL (not timed), and the full-output gather on its own
     from HyGrid.dist import gather_checksums, gather_to_root, image_checksums
     cs = image_checksums(y)
@@ -421,7 +457,8 @@ def main():
                        "height": H, "width": W, "parallelism": f"dp{world}",
                        "fused": not args.unfused},
             "kernels": kernels, "roofline": roofline, "cpu_baseline": cpu,
-            "unfused": compare, "roundtrip": roundtrip, "pyramid": pyramid, "gather": gather, "checksum": checksum,
+            "unfused": compare, "roundtrip": roundtrip, "pyramid": pyramid, "wide_conv": wide,
+            "gather": gather, "checksum": checksum,
             "device": torch.cuda.get_device_name(dev),
         }
         print(json.dumps(line), flush=True)

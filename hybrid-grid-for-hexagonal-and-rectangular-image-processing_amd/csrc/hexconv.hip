@@ -238,6 +238,10 @@ int launch_conv_stream(const void* x, const float* k, const float* b, void* y, i
                        int y_dtype, int64_t B, int C, int O, int64_t h, int64_t w, int p,
                        int groups, int off, double pad_value, const Epilogue& epi,
                        hipStream_t st);   // conv_stream.hip
+int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_dtype,
+                  int y_dtype, int64_t B, int64_t C, int64_t O, int64_t h, int64_t w, int radius,
+                  int stride, int padding, int dilation, int groups, int off, int pad_mode,
+                  double pad_value, const Epilogue& epi, hipStream_t st);   // conv_mfma.hip
 
 }  // namespace hg
 
@@ -291,6 +295,12 @@ int hg_hexconv2d_epilogue(const void* x, const void* kernel, const void* bias, v
         st = launch_conv_stream(x, (const float*)kernel, (const float*)bias, y, x_dtype, y_dtype,
                                 batch, (int)in_channels, (int)out_channels, h, w, padding,
                                 groups, even_odd_offset & 1, pad_value, epi, s);
+        if (st != HG_EUNSUP) return st;
+    }
+    if (w_dtype == HG_F32) {   // wide channels: implicit GEMM on the f32 matrix cores
+        st = conv_mfma_try(x, (const float*)kernel, (const float*)bias, y, x_dtype, y_dtype,
+                           batch, in_channels, out_channels, h, w, radius, stride, padding,
+                           dilation, groups, even_odd_offset & 1, pad_mode, pad_value, epi, s);
         if (st != HG_EUNSUP) return st;
     }
     G.B = batch; G.C = in_channels; G.O = out_channels; G.h = h; G.w = w;

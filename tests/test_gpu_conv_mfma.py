@@ -1,0 +1,125 @@
+"""GPU parity of the wide-channel HexConv2d path (csrc/conv_mfma.hip: implicit GEMM on
+v_mfma_f32_16x16x4_f32, dense radius 2 / stride 1 / dilation 1, C >= 8, O >= 16) against
+the fp64 oracle (oracle/hg_oracle.c, pinned to HexFrames.py:96-169 by
+tests/golden/hexconv.npz) at the north_star fp32 tolerance (rtol 1e-5, atol 1e-5*max|ref|),
+and against the generic LDS kernel (HYGRID_CONV_MFMA=0) for 16-bit outputs and the fused
+HexConvModule epilogue."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover
+    pytest.skip("needs a HIP device", allow_module_level=True)
+
+from HyGrid import ops  # noqa: E402
+
+DEV = torch.device("cuda:0")
+
+
+def _generic(fn, *args, **kw):
+    old = os.environ.get("HYGRID_CONV_MFMA")
+    os.environ["HYGRID_CONV_MFMA"] = "0"
+    try:
+        out = fn(*args, **kw)
+        torch.cuda.synchronize()
+        return out
+    finally:
+        if old is None:
+            del os.environ["HYGRID_CONV_MFMA"]
+        else:
+            os.environ["HYGRID_CONV_MFMA"] = old
+
+
+def _weights(O_, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    bound = 1.0 / np.sqrt(7 * C)
+    k = ((torch.rand((O_, C, 1, 7), generator=g) * 2 - 1) * bound).to(DEV)
+    b = ((torch.rand((O_,), generator=g) * 2 - 1) * bound).to(DEV)
+    return k, b
+
+
+CASES = [  # (B, C, O, h, w)
+    (2, 8, 16, 9, 10), (1, 16, 16, 33, 70), (1, 32, 64, 20, 130), (2, 64, 64, 17, 64),
+    (1, 13, 20, 12, 21), (1, 24, 100, 11, 75), (1, 70, 33, 6, 9),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("pad", [0, 1, 2])
+@pytest.mark.parametrize("off", [0, 1])
+def test_mfma_conv_fp32_vs_oracle(case, pad, off):
+    B, C, O_, h, w = case
+    k, b = _weights(O_, C, h * 13 + w + pad)
+    rng = np.random.default_rng(h + w * 3 + off)
+    x = rng.random((B, C, h, w)).astype(np.float32) - 0.5
+    y = ops.hexconv2d(torch.from_numpy(x).to(DEV), k, b, off, 2, padding=pad,
+                      out_dtype=torch.float32).cpu().numpy()
+    ref = O.hexconv2d(x.astype(np.float64), k.cpu().double().numpy(),
+                      b.cpu().double().numpy(), off, 2, padding=pad)
+    scale = max(np.abs(ref).max(), 1e-30)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5 * scale)
+
+
+@pytest.mark.parametrize("mode", ["constant", "reflect", "replicate", "circular"])
+def test_mfma_conv_pad_modes_vs_oracle(mode):
+    B, C, O_, h, w = 1, 16, 32, 14, 40
+    k, b = _weights(O_, C, 7)
+    rng = np.random.default_rng(5)
+    x = rng.random((B, C, h, w)).astype(np.float32)
+    pv = 0.3 if mode == "constant" else 0.0
+    y = ops.hexconv2d(torch.from_numpy(x).to(DEV), k, b, 0, 2, padding=1, padding_mode=mode,
+                      padding_value=pv, out_dtype=torch.float32).cpu().numpy()
+    ref = O.hexconv2d(x.astype(np.float64), k.cpu().double().numpy(), b.cpu().double().numpy(),
+                      0, 2, padding=1, padding_mode=mode, padding_value=pv)
+    scale = max(np.abs(ref).max(), 1e-30)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5 * scale)
+
+
+@pytest.mark.parametrize("dt_in,dt_out", [(torch.bfloat16, torch.bfloat16),
+                                          (torch.bfloat16, torch.float32),
+                                          (torch.float16, torch.float16),
+                                          (torch.float32, torch.bfloat16)])
+def test_mfma_conv_16bit_vs_generic(dt_in, dt_out):
+    B, C, O_, h, w = 2, 32, 48, 30, 100
+    k, b = _weights(O_, C, 3)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = (torch.rand((B, C, h, w), generator=g, device=DEV) - 0.5).to(dt_in)
+    y = ops.hexconv2d(x, k, b, 0, 2, padding=1, out_dtype=dt_out)
+    ref = _generic(ops.hexconv2d, x, k, b, 0, 2, padding=1, out_dtype=dt_out)
+    ulp = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11, torch.float32: 1e-5}[dt_out]
+    scale = float(ref.float().abs().max())
+    torch.testing.assert_close(y.float(), ref.float(), rtol=ulp, atol=ulp * scale)
+
+
+@pytest.mark.parametrize("act", ["ReLU", "LeakyReLU", "Sigmoid"])
+def test_mfma_hexconvmodule_epilogue_vs_generic(act):
+    """HexConvModule's fused conv + eval BatchNorm + activation on the MFMA kernel."""
+    from HyGrid.HexModules import HexConvModule
+    torch.manual_seed(2)
+    m = HexConvModule(16, 32, 0, 2, padding=1, norm_cfg=dict(type="BN"),
+                      act_cfg=dict(type=act)).to(DEV).eval()
+    with torch.no_grad():
+        m.norm.running_mean.uniform_(-0.2, 0.2)
+        m.norm.running_var.uniform_(0.5, 1.5)
+        x = torch.rand((2, 16, 24, 50), device=DEV)
+        y = m(x)
+        ref = _generic(m, x)
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+
+
+def test_mfma_conv_nan_positions_match_generic():
+    B, C, O_, h, w = 1, 16, 16, 20, 70
+    k, b = _weights(O_, C, 4)
+    x = torch.rand((B, C, h, w), device=DEV)
+    x[0, 3, 0, 5] = float("nan")
+    x[0, 7, 19, 69] = float("inf")
+    y = ops.hexconv2d(x, k, b, 1, 2, padding=1, out_dtype=torch.float32)
+    ref = _generic(ops.hexconv2d, x, k, b, 1, 2, padding=1, out_dtype=torch.float32)
+    assert torch.equal(torch.isnan(y), torch.isnan(ref))
+    assert torch.equal(torch.isinf(y), torch.isinf(ref))
