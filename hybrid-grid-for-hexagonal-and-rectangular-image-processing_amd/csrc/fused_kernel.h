@@ -53,6 +53,12 @@ constexpr int FU_LUT = FU_RB + 2;     // u rows band_begin-1 .. band_begin+RB
 #ifndef FU_DRAIN
 #define FU_DRAIN 1                    // drain the prologue's loads before the row loop
 #endif
+#ifndef FU_RC
+#define FU_RC 1                       // per-band row-class specialisation of the r2h rows
+#endif
+#ifndef FU_FOLD
+#define FU_FOLD 1                     // MD 0: the h2r 0.75 folded into the conv weights
+#endif
 
 struct FusedGeom {
     int64_t B;
@@ -190,6 +196,21 @@ void k_fused(const Tin* __restrict__ x,
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): own-wave LDS writes
     __builtin_amdgcn_wave_barrier();
+    // Row class of the band (uniform): RC 1 if every u row blends rect rows r-1, r
+    // (table c == 0), RC 2 if rows r, r+1 (a == 0): two terms per vertical blend instead
+    // of three.  A same-size lattice switches class once, in the middle band.
+    int rc = 0;
+    if (MD == 0 && FU_RC) {
+        bool has_a = false, has_c = false;
+        for (int e = lane; e < FU_LUT; e += 64) {
+            const float4 t = lut[e];
+            has_a |= t.x != 0.f;
+            has_c |= t.z != 0.f;
+        }
+        const bool any_a = __builtin_amdgcn_ballot_w64(has_a) != 0;
+        const bool any_c = __builtin_amdgcn_ballot_w64(has_c) != 0;
+        rc = !any_c ? 1 : (!any_a ? 2 : 0);
+    }
 
     // ---- per-lane column weights --------------------------------------------
     // r2h (geometry_np.py:441-449, 514-517): u[q] = sum_k wr_k[q] v[q+k], k = -1..1
@@ -247,14 +268,22 @@ void k_fused(const Tin* __restrict__ x,
     // FMA operand is a VGPR: an opaque per-lane zero offset makes these vector loads.
     int vz = 0;
     asm volatile("" : "+v"(vz));
+    // MD 0 with FU_FOLD: the exact same-size h2r is 0.75 z[b] + 0.25 z[b +- 1]
+    // (geometry_np.py:347-354); with the conv weights and bias pre-scaled by 0.75 it is
+    // z'[b] + z'[b +- 1] / 3, one FMA per output column instead of two (fp32-rounding
+    // level difference, well inside the 1e-5 tolerance)
+    constexpr bool FOLD = FU_FOLD && MD == 0;
+    const float ws_ = FOLD ? 0.75f : 1.f;
     float wk[O * CG * 7];
 #pragma unroll
-    for (int i = 0; i < O * CG * 7; ++i) wk[i] = kern[i + (FU_WSGPR ? 0 : vz)];
+    for (int i = 0; i < O * CG * 7; ++i) wk[i] = kern[i + (FU_WSGPR ? 0 : vz)] * ws_;
     float bv[O];
 #pragma unroll
-    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] : 0.f;
+    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] * ws_ : 0.f;
     float c75 = 0.75f, c25 = 0.25f;     // h2r weights as VGPR operands, not literals
-    asm volatile("" : "+v"(c75), "+v"(c25));
+    float c13 = 1.f / 3.f;
+    asm volatile("" : "+v"(c75), "+v"(c25), "+v"(c13));
+    const float wn_f = wn_o != 0.f ? c13 : 0.f, wp_f = wp_e != 0.f ? c13 : 0.f;
     unsigned hi16 = 0xffff0000u;
     asm volatile("" : "+v"(hi16));
 
@@ -266,8 +295,9 @@ void k_fused(const Tin* __restrict__ x,
     const bool any_r = __builtin_amdgcn_ballot_w64(we[2] != 0.f || wo_[2] != 0.f) != 0;
     const int cd = !FU_CD ? 0 : (!any_r ? 1 : (!any_l ? 2 : 0));
 
-    auto run = [&](auto CDc) {
+    auto run = [&](auto CDc, auto RCc) {
         constexpr int CD = decltype(CDc)::value;
+        constexpr int RC = decltype(RCc)::value;
         // ---- state -----------------------------------------------------------------
         Raw raw[6][C];                      // rect rows in flight, slot (row - s0) % 6
         float XE[3][C], XO[3][C];           // rect rows as f32, slot (row - s0) % 3
@@ -305,8 +335,17 @@ void k_fused(const Tin* __restrict__ x,
             } else
     #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const float ve = fmaf(L.z, XE[S2][c], fmaf(L.y, XE[S1][c], L.x * XE[S0][c]));
-                const float vo = fmaf(L.z, XO[S2][c], fmaf(L.y, XO[S1][c], L.x * XO[S0][c]));
+                float ve, vo;
+                if constexpr (RC == 1) {            // rect rows r-1, r
+                    ve = fmaf(L.y, XE[S1][c], L.x * XE[S0][c]);
+                    vo = fmaf(L.y, XO[S1][c], L.x * XO[S0][c]);
+                } else if constexpr (RC == 2) {     // rect rows r, r+1
+                    ve = fmaf(L.z, XE[S2][c], L.y * XE[S1][c]);
+                    vo = fmaf(L.z, XO[S2][c], L.y * XO[S1][c]);
+                } else {
+                    ve = fmaf(L.z, XE[S2][c], fmaf(L.y, XE[S1][c], L.x * XE[S0][c]));
+                    vo = fmaf(L.z, XO[S2][c], fmaf(L.y, XO[S1][c], L.x * XO[S0][c]));
+                }
                 if constexpr (CD == 1) {            // taps q-1, q
                     ue[c] = fmaf(we[1], ve, we[0] * f_prev(vo));
                     uo[c] = fmaf(wo_[1], vo, wo_[0] * ve);
@@ -377,6 +416,12 @@ void k_fused(const Tin* __restrict__ x,
                 if constexpr (MD == 1) {            // HexConv2d output row as is
                     oe = ze;
                     oo = zo;
+                } else if constexpr (FOLD && (PH & 1) == 0) {   // z' = 0.75 z
+                    oe = fmaf(c13, zo, ze);
+                    oo = fmaf(wn_f, f_next(ze), zo);
+                } else if constexpr (FOLD) {
+                    oe = fmaf(wp_f, f_prev(zo), ze);
+                    oo = fmaf(c13, ze, zo);
                 } else if constexpr ((PH & 1) == 0) {      // 0.75 z[b] + 0.25 z[b+1]
                     oe = fmaf(c25, zo, c75 * ze);
                     oo = fmaf(wn_o, f_next(ze), c75 * zo);
@@ -518,12 +563,15 @@ void k_fused(const Tin* __restrict__ x,
         }
     };
     if constexpr (MD == 1) {
-        (void)cd;
-        run(IC<0>{});
+        (void)cd; (void)rc;
+        run(IC<0>{}, IC<0>{});
     } else {
-        if (FU_CD && cd == 1) run(IC<1>{});
-        else if (FU_CD && cd == 2) run(IC<2>{});
-        else run(IC<0>{});
+        // the common classes get their own loop; mixed windows / bands run the generic one
+        if (FU_CD && cd == 1 && rc == 1) run(IC<1>{}, IC<1>{});
+        else if (FU_CD && cd == 1 && rc == 2) run(IC<1>{}, IC<2>{});
+        else if (FU_CD && cd == 2 && rc == 1) run(IC<2>{}, IC<1>{});
+        else if (FU_CD && cd == 2 && rc == 2) run(IC<2>{}, IC<2>{});
+        else run(IC<0>{}, IC<0>{});
     }
 }
 
