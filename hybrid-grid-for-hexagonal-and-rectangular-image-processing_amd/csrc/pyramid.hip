@@ -325,7 +325,9 @@ __global__ __launch_bounds__(PY_THREADS) void k_pyr_level(const Tin* __restrict_
                 wm[j] = xcol[rb * PY_XP + j];
                 w0[j] = xcol[(rb + 1) * PY_XP + j];
             }
-            // one Y row of parity PAR (tap columns as in fused_kernel.h), then slide
+            // one Y row of parity PAR (tap columns as in fused_kernel.h), then slide (a
+            // 3-row register ring unrolled by 6 instead needs ~25 more VGPRs: 3 waves per
+            // SIMD instead of 4, and ran slower)
             auto yrow = [&](int rr, auto PARc) {
                 constexpr int PAR = decltype(PARc)::value;
 #pragma unroll
@@ -366,7 +368,11 @@ __global__ __launch_bounds__(PY_THREADS) void k_pyr_level(const Tin* __restrict_
                 dp[(int64_t)a * G.w1 + b] = (Tout)v;
             }
         }
-        __syncthreads();
+        // Without from_rect no barrier here: the next plane's staging writes only the X
+        // tile (last read by this plane's Y stage, before the barrier above), and its
+        // first barrier orders this Z stage's Y reads before the next Y stage's writes.
+        // from_rect stages the rect tile into the Y tile's buffer: wait for every Z read.
+        if constexpr (FROM_RECT) __syncthreads();
     };
     for (int64_t p = p0; p < p1; p += 2) {
         plane(p, pfa);
