@@ -94,8 +94,8 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
     if ((w & 1) || (w1 & 1) || w < 2 || h1 < 1) return HG_EUNSUP;   // dword column pairs
     if (x_dtype != HG_BF16 && x_dtype != HG_F16 && x_dtype != HG_F32) return HG_EUNSUP;
     if (y_dtype != HG_BF16 && y_dtype != HG_F16 && y_dtype != HG_F32) return HG_EUNSUP;
-    if (C * h * w * 4 >= ((int64_t)1 << 31) || O * h2 * w2 * 4 >= ((int64_t)1 << 31))
-        return HG_EUNSUP;                             // 32-bit buffer offsets
+    if (C * h * w * 8 >= ((int64_t)1 << 31) || O * h2 * w2 * 4 >= ((int64_t)1 << 31))
+        return HG_EUNSUP;   // 32-bit buffer offsets, incl. the past-the-range zero loads
     const Geom g = make_r2h(h, w, h1, w1);
     if (!fused_geometry_ok(g)) return HG_EUNSUP;
     FusedGeom F;

@@ -43,8 +43,8 @@ int fused_conv_try(const void* x, const float* kernel, const float* bias, void* 
     }
     if (epilogue || padding != 1 || pad_value != 0.0) return HG_EUNSUP;
     if ((w & 1) || w < 2 || h < 1 || batch < 1) return HG_EUNSUP;   // dword column pairs
-    if (C * h * w * 4 >= ((int64_t)1 << 31) || O * h * w * 4 >= ((int64_t)1 << 31))
-        return HG_EUNSUP;                             // 32-bit buffer offsets
+    if (C * h * w * 8 >= ((int64_t)1 << 31) || O * h * w * 4 >= ((int64_t)1 << 31))
+        return HG_EUNSUP;   // 32-bit buffer offsets, incl. the past-the-range zero loads
     FusedGeom F = {};
     F.B = batch;
     F.h = F.h1 = F.h2 = (int)h;

@@ -119,3 +119,39 @@ def test_non_identity_geometry_falls_back():
         y = rect_hex_conv_rect(x, conv, (32, 48), (64, 96))
     ref = oracle_chain(x, conv, (32, 48), (64, 96))
     close(y.cpu().numpy(), ref, 1e-5)
+
+
+@pytest.mark.parametrize("off", [0, 1])
+def test_fused_nonfinite_inputs_stay_local(off):
+    """Inf / NaN inputs inside the raster, at the 120-column window edges and the 126-row
+    band edges.  The fused kernel evaluates a fixed tap set per column / row class, so a
+    tap whose weight is exactly 0 for one column is still multiplied (0 * Inf = NaN) where
+    the reference never reads it; conversely the reference multiplies the same-size h2r's
+    zero-weight third vertex (geometry_np.py:347-354) where the fused kernel has no tap.
+    Non-finite inputs therefore may reach outputs up to 3 samples away differently from the
+    reference (the operator chain propagates them exactly).  Asserted:
+    every output farther than 3 rows / columns from a non-finite input is finite and
+    matches the fp64 oracle chain within 1e-5 — the damage stays local."""
+    torch.manual_seed(3)
+    conv = HexConv2d(3, 3, off, 2, padding=1, bias=True).to(DEV)
+    B, C, H, W = 1, 3, 130, 256
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.rand((B, C, H, W), generator=g, device=DEV)
+    inf, nan = float("inf"), float("nan")
+    pts = [(0, 3, 50, inf), (1, H - 4, 77, -inf), (2, 40, 3, inf), (0, 90, W - 4, -inf),
+           (1, 20, 119, nan), (2, 125, 121, inf), (0, 0, 0, inf), (2, H - 1, W - 1, nan)]
+    for c, r, q, v in pts:
+        x[0, c, r, q] = v
+    with torch.no_grad():
+        y = ops.pipeline_r2h_conv_h2r(x, conv.kernel, conv.bias, None, None, 1, 1, off, 0.0,
+                                      torch.float32)
+    assert y is not None
+    ref = oracle_chain(x, conv, (H, W), (H, W))
+    got = y.double().cpu().numpy()
+    near = np.zeros((H, W), bool)
+    for _, r, q, _ in pts:
+        near[max(r - 3, 0):r + 4, max(q - 3, 0):q + 4] = True
+    far = np.broadcast_to(~near, got.shape)
+    assert np.isfinite(ref[far]).all() and np.isfinite(got[far]).all()
+    scale = np.abs(ref[far]).max()
+    np.testing.assert_allclose(got[far], ref[far], rtol=1e-5, atol=1e-5 * scale)
