@@ -235,8 +235,10 @@ def main():
                 traffic_note = (f"{args.pmc_json} profiled kernel sources "
                                 f"{pmc.get('kernel_source_digest')}, this tree is {here}")
             elif dom in pmc.get("kernels", {}):
-                traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"]
-                traffic_note = f"rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE, kernel sources {here}"
+                # per launch at the profiled batch, scaled to this run's batch
+                traffic = pmc["kernels"][dom]["hbm_bytes_per_launch"] * B / pmc.get("batch", B)
+                traffic_note = (f"rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE at batch "
+                                f"{pmc.get('batch', B)}, kernel sources {here}")
         except Exception as exc:  # keep the bench line even if the file is malformed
             log("pmc json unreadable:", exc)
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),

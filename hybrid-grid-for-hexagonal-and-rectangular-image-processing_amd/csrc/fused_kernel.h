@@ -249,15 +249,9 @@ void k_fused(const Tin* __restrict__ x,
         (void*)(x + b * C * cstride), (short)0, (int)(C * cstride * (int64_t)sizeof(Tin)), 0x00020000);
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(y + b * O * ostride), (short)0, (int)(O * ostride * (int64_t)sizeof(Tout)), 0x00020000);
-    // Rows / columns outside the raster load 0 through the buffer's range check (an offset
-    // past num_records): the reference's masked gathers read 0 there
-    // (geometry_np.py:478-486), and HexConv2d's constant-0 padding is the same zeros.
-    // (Clamped loads times a zero weight would turn an edge Inf into a NaN.)  w is even
-    // and ce is even, so a lane's two columns are both inside or both outside.
-    const int lc = ce;
+    const int lc = min(max(ce, 0), F.w - 2);            // clamped even load column
     // one VGPR offset per lane; the plane of a channel is an SGPR offset
-    const unsigned xoff = (lc >= 0 && lc < F.w) ? (unsigned)lc * (unsigned)sizeof(Tin) : 0x80000000u;
-    const unsigned xoob = (unsigned)(C * cstride * (int64_t)sizeof(Tin));   // >= num_records
+    const unsigned xoff = (unsigned)lc * (unsigned)sizeof(Tin);
     const unsigned yoff = own ? (unsigned)ce * (unsigned)sizeof(Tout) : 0x80000000u;
     const unsigned xplane = (unsigned)(cstride * (int64_t)sizeof(Tin));
     const unsigned yplane = (unsigned)(ostride * (int64_t)sizeof(Tout));
@@ -265,8 +259,7 @@ void k_fused(const Tin* __restrict__ x,
     const unsigned yrow = (unsigned)F.w2 * (unsigned)sizeof(Tout);
     auto row_off = [&](int k) -> unsigned {             // clamped rect row (SALU)
         if (FU_NOMEM) return 0u;
-        return (unsigned)__builtin_amdgcn_readfirstlane(
-            (int)((k >= 0 && k < F.h) ? (unsigned)k * xrow : xoob));
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(k, 0), F.h - 1) * xrow));
     };
 
     // ---- weights and bias in VGPRs -------------------------------------------------
@@ -333,11 +326,11 @@ void k_fused(const Tin* __restrict__ x,
             constexpr int PC = 1 - PB;              // parity of conv row r
             float ue[C], uo[C];
             if constexpr (MD == 1) {                // u = input row, 0 outside (padding 1, value 0)
-                (void)colin;                        // padding rows / columns loaded as 0
+                const bool in_ = colin && L.y != 0.f;
     #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    ue[c] = XE[S1][c];
-                    uo[c] = XO[S1][c];
+                    ue[c] = in_ ? XE[S1][c] : 0.f;
+                    uo[c] = in_ ? XO[S1][c] : 0.f;
                 }
             } else
     #pragma unroll

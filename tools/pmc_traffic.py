@@ -23,9 +23,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGES = {   # json key -> (prof_pipeline stage, kernel-name substring)
     "pipeline_r2h_conv_h2r": ("fused", "k_fused"),
-    "rect_to_hex": ("r2h", "k_resample"),
+    "rect_to_hex": ("r2h", "k_r2h_stream"),
     "hexconv2d": ("conv", "k_hexconv"),
-    "hex_to_rect": ("h2r", "k_resample"),
+    "hex_to_rect": ("h2r", "k_h2r_stream"),
     "calib_torch_copy": ("copy", "__amd_rocclr_copyBuffer"),
     "calib_r2h_nearest": ("r2h_nearest", "k_resample_nearest"),
 }
