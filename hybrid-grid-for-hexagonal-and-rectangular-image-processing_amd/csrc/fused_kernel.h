@@ -14,10 +14,27 @@
 namespace hg {
 
 constexpr int FU_THREADS = 256;       // 4 independent waves per workgroup
-constexpr int FU_HL = 4;              // halo columns on the left of a window
-constexpr int FU_OWN = 120;           // owned columns per 128-column window
-constexpr int FU_RB = 126;            // output rows per band (multiple of 6)
-constexpr int FU_LUT = FU_RB + 2;     // u rows band_begin-1 .. band_begin+RB
+#ifndef FU_HL_
+#define FU_HL_ 4
+#endif
+#ifndef FU_OWN_
+#define FU_OWN_ 120
+#endif
+constexpr int FU_HL = FU_HL_;         // halo columns on the left of a window
+constexpr int FU_OWN = FU_OWN_;       // owned columns per 128-column window
+// Output rows per band (multiple of 6), MD 0 / MD 1.  Shorter bands than the 126 of
+// round 1 measured faster (in-process A/B on 4K bf16 b128, tools/ab_fused.py /
+// tools/ab_ops.py): pipeline 3.00 -> 2.83 ms at 66, HexConv2d 3.19 -> 2.73 ms at 18.
+#ifndef FU_RB_
+#define FU_RB_ 66
+#endif
+#ifndef FU_RB_CONV_
+#define FU_RB_CONV_ 18
+#endif
+constexpr int FU_RB = FU_RB_;
+constexpr int FU_RB_CONV = FU_RB_CONV_;
+constexpr int FU_LUT = (FU_RB > FU_RB_CONV ? FU_RB : FU_RB_CONV) + 2;   // row table capacity
+__host__ __device__ constexpr int fu_rb(int md) { return md == 1 ? FU_RB_CONV : FU_RB; }
 
 // Tuning knobs (compile-time; tools/build_fvariant.sh builds variants of this file).
 #ifndef FU_PD
@@ -174,11 +191,12 @@ void k_fused(const Tin* __restrict__ x,
     const int win = grp * GW + wslot;             // may be >= nwin: runs, owns nothing
     const int W0 = win * FU_OWN - FU_HL;
     const int ce = W0 + 2 * lane;                 // this lane's even column; odd = ce + 1
-    const int s0 = band * FU_RB;                  // first output row of the band
-    const int s1 = min(s0 + FU_RB, F.h2);
+    constexpr int RB = fu_rb(MD), NLUT = RB + 2;  // rows per band, u rows band_begin-1 .. +RB
+    const int s0 = band * RB;                     // first output row of the band
+    const int s1 = min(s0 + RB, F.h2);
 
     // ---- row table (fp64 lattice math, geometry_np.py:440-486) -------------
-    for (int e = lane; e < FU_LUT; e += 64) {
+    for (int e = lane; e < NLUT; e += 64) {
         const int r = s0 - 1 + e;                 // u row
         float4 t = {0.f, 0.f, 0.f, 0.f};
         if (MD == 1) {
@@ -202,7 +220,7 @@ void k_fused(const Tin* __restrict__ x,
     int rc = 0;
     if (MD == 0 && FU_RC) {
         bool has_a = false, has_c = false;
-        for (int e = lane; e < FU_LUT; e += 64) {
+        for (int e = lane; e < NLUT; e += 64) {
             const float4 t = lut[e];
             has_a |= t.x != 0.f;
             has_c |= t.z != 0.f;
@@ -513,7 +531,7 @@ void k_fused(const Tin* __restrict__ x,
             convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row a2+2
             issue(IC<(PH + 2 + PD) % 6>{}, a2 + 2 + PD);
             const float4 L = lnext;
-            lnext = lut[min(a2 - s0 + 3, FU_LUT - 1)];
+            lnext = lut[min(a2 - s0 + 3, NLUT - 1)];
             urow(PHc, L, std::true_type{}, std::true_type{});           // u row a2+1
             out_row(PHc, SBc, a2);
         };

@@ -1,0 +1,341 @@
+// pyramid_stream.hip — row-streaming form of one hex-pyramid level (BASELINE config 5):
+//     Z = hexresize(HexConv2d_depthwise(X), (h1, w1))   for a 2x downsample
+// The reference runs the two stages as separate calls: HexConv2d(C, C, off, 2,
+// padding=1, groups=C) (HexFrames.py:96-169) and hexresize (geometry_np.py:520-681,
+// 'linear').  k_pyr_level (pyramid.hip) stages 2-D tiles in LDS with two barriers per
+// plane and spends most of its wave time parked; this kernel keeps everything in
+// registers, like the fused pipeline (fused_kernel.h):
+//
+//  * one wavefront owns a window of 128 input columns (lane l <-> hex columns
+//    W0 + 2l, W0 + 2l + 1, one dword of 16-bit input) of one image, all C channels,
+//    and walks a band of output rows; lanes 2..61 own output column b = W0/2 + l;
+//  * output row a needs conv rows R0 = i_n(a), R1 = R0 + 1 (geometry_np.py:601-620),
+//    i.e. input rows R0 - 1 .. R0 + 2; for a 2x downsample i_n(a) - 2a is 0 or 1, so a
+//    step consumes two new input rows, loaded two steps ahead into a 10-row register
+//    ring (every input row is loaded once);
+//  * conv rows R0, R1 at the lane's two columns: 7 taps x 2 columns x 2 rows, the
+//    neighbour columns one DPP wave shift away (zeros outside the raster = padding 1);
+//  * the triangle (geometry_np.py:612-648): p1 = (R0, c0), p2 = (R1, c1) if i_f > j_f
+//    else (R0, c0 + 1), p3 = (R1, c1 + 1) with c0 = j_n - (i_n+1)//2,
+//    c1 = j_n - (i_n+2)//2 (fp64 lattice per lane and row, the reference's expression
+//    order); c0 - 2b in {-1, 0, 1} (host-checked), so every vertex is the lane's own
+//    conv value or a neighbour lane's, picked with selects; vertices outside the raster
+//    read 0 (:636-648);
+//  * weights: the barycentric coordinates of the triangle in the lattice's (i, j) index
+//    frame, where the reference's Cartesian frame (:651-656) is an affine image of it:
+//    flag: (1 - i_f, i_f - j_f, j_f), else (1 - j_f, j_f - i_f, i_f) — the reference's
+//    S1/S, S2/S, S3/S (:673-678) up to fp64 rounding, then rounded to fp32.
+// Out-of-domain calls (other size ratios, odd widths, C not in {1, 3}) return HG_EUNSUP
+// and k_pyr_level runs.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+#include "lattice.h"
+
+namespace hg {
+
+constexpr int PS_THREADS = 256;    // 4 waves = 4 adjacent windows
+constexpr int PS_OWN = 60;         // output columns per window (lanes 2..61)
+#ifndef PS_RB_
+#define PS_RB_ 30
+#endif
+constexpr int PS_RB = PS_RB_;      // output rows per band (multiple of 5: ring period)
+
+struct PyrStreamGeom {
+    int64_t B;
+    int h, w, h1, w1;
+    int nwin, nband;
+    Axis xs, ys;                   // hexresize lattice axes (geometry_np.py:570-582)
+    const float* taps;             // [C][7]
+    const float* bias;             // [C] or null
+};
+
+__device__ __forceinline__ float ps_prev(float v) {   // v[l-1], 0 at lane 0
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+        __builtin_bit_cast(int, v), 0x138 /*wave_shr:1*/, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float ps_next(float v) {   // v[l+1], 0 at lane 63
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+        __builtin_bit_cast(int, v), 0x130 /*wave_shl:1*/, 0xf, 0xf, true));
+}
+
+// r=2, padding-1 taps (HexFrames.py:108-118 in the type-1 frame; as fused_kernel.h):
+// tap t of a conv row of parity par reads row +(ii-1), column +shift (shift in -1..2)
+__host__ __device__ constexpr int ps_tap_ii(int t) { return t < 2 ? 0 : (t < 5 ? 1 : 2); }
+__host__ __device__ constexpr int ps_tap_col(int t) {
+    return t < 2 ? 1 + 2 * t : (t < 5 ? 2 * (t - 2) : 1 + 2 * (t - 5));
+}
+__host__ __device__ constexpr int ps_tap_shift(int t, int par, int op) {
+    return ((1 + par + ps_tap_col(t) - ((((par + ps_tap_ii(t)) & 1) + op) & 1)) >> 1) - 1;
+}
+template <int N> using PIC = std::integral_constant<int, N>;
+
+template <int OP, int C, typename Tin, typename Tout>
+__global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict__ x,
+                                                           Tout* __restrict__ y,
+                                                           PyrStreamGeom G) {
+    static_assert(sizeof(Tin) == 2, "16-bit input (one dword = the lane's two columns)");
+    const int lane = threadIdx.x & 63;
+    const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
+    const int ngrp = (G.nwin + 3) / 4;
+    const int grp = (int)(blk % ngrp);
+    const int64_t rest = blk / ngrp;
+    const int band = (int)(rest % G.nband);
+    const int64_t img = rest / G.nband;
+    if (img >= G.B) return;                          // uniform per workgroup
+    const int win = grp * 4 + wslot;                 // may be >= nwin: runs, owns nothing
+    const int W0 = win * (2 * PS_OWN) - 4;           // input column of lane 0 (even)
+    const int ce = W0 + 2 * lane;                    // lane's even column; odd = ce + 1
+    const int bo = W0 / 2 + lane;                    // lane's output column
+    const int a0 = band * PS_RB, a1 = min(a0 + PS_RB, G.h1);
+    const bool own = lane >= 2 && lane < 2 + PS_OWN && bo < G.w1 && win < G.nwin;
+    const bool colin = ce >= 0 && ce < G.w;          // w even: the dword is in or out
+
+    // ---- per-lane lattice constants (fp64, geometry_np.py:570-602) ------------------
+    const double yv = axis_at(G.ys, min(max(bo, 0), G.w1 - 1));   // y_ of this column
+    const double cw = ((double)G.w - 0.5) * 0.5;
+    const double ch = (double)(G.h - 1) * 0.5;
+
+    // ---- buffers -------------------------------------------------------------------
+    const int64_t ipl = (int64_t)G.h * G.w, opl = (int64_t)G.h1 * G.w1;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + img * C * ipl), (short)0, (int)(C * ipl * (int64_t)sizeof(Tin)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(y + img * C * opl), (short)0, (int)(C * opl * (int64_t)sizeof(Tout)), 0x00020000);
+    const int lc = min(max(ce, 0), G.w - 2);
+    const unsigned xoff = (unsigned)lc * (unsigned)sizeof(Tin);
+    const unsigned yoff = own ? (unsigned)bo * (unsigned)sizeof(Tout) : 0x80000000u;
+    const unsigned xplane = (unsigned)(ipl * (int64_t)sizeof(Tin));
+    const unsigned yplane = (unsigned)(opl * (int64_t)sizeof(Tout));
+    const unsigned xrow = (unsigned)G.w * (unsigned)sizeof(Tin);
+    const unsigned yrow = (unsigned)G.w1 * (unsigned)sizeof(Tout);
+
+    // taps and bias in VGPRs (an SGPR operand halves the VALU issue rate on gfx950)
+    int vz = 0;
+    asm volatile("" : "+v"(vz));
+    float wk[C * 7], bv[C];
+#pragma unroll
+    for (int i = 0; i < C * 7; ++i) wk[i] = G.taps[i + vz];
+#pragma unroll
+    for (int c = 0; c < C; ++c) bv[c] = G.bias ? G.bias[c + vz] : 0.f;
+
+    // ---- input ring: rows 2*a0 - 1 + k in slot k % 10 --------------------------------
+    const int rb0 = 2 * a0 - 1;
+    unsigned raw[10][C];
+    auto issue = [&](auto SLc, int r) {
+        constexpr int SL = decltype(SLc)::value;
+        const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane(
+            (int)((unsigned)min(max(r, 0), G.h - 1) * xrow));
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            raw[SL][c] = __builtin_amdgcn_raw_buffer_load_b32(xrs, xoff, so + c * xplane, 0);
+    };
+    // input row -> f32 pair, zero outside the raster (the conv's constant-0 padding)
+    auto xrowf = [&](auto SLc, int r, int c, float& e, float& o) {
+        constexpr int SL = decltype(SLc)::value;
+        const bool in = colin && r >= 0 && r < G.h;
+        const unsigned v = raw[SL][c];
+        e = in ? (float)__builtin_bit_cast(Tin, (unsigned short)(v & 0xffffu)) : 0.f;
+        o = in ? (float)__builtin_bit_cast(Tin, (unsigned short)(v >> 16)) : 0.f;
+    };
+
+    // one output row a (ring offset K = a - a0 mod 5, static); E = i_n(a) - 2a
+    auto step = [&](auto Kc, auto Ec, int a, const double i_, int i_n) {
+        constexpr int K = decltype(Kc)::value, E = decltype(Ec)::value;
+        // lattice of this (row, lane) (geometry_np.py:601-623)
+        const double i_f = i_ - (double)(float)i_n;
+        const double j_ = 0.5 * i_ + yv + cw;
+        const int j_n = (int)j_;
+        const double j_f = j_ - (double)(float)j_n;
+        const bool flag = i_f > j_f;
+        const float wa = (float)(flag ? 1.0 - i_f : 1.0 - j_f);
+        const float wb = (float)(flag ? i_f - j_f : j_f - i_f);
+        const float wg = (float)(flag ? j_f : i_f);
+        const int R0 = i_n, R1 = i_n + 1;
+        const int c0 = j_n - (i_n + 1) / 2, c1 = j_n - (i_n + 2) / 2;
+        const int d0 = c0 - 2 * bo, d1 = c1 - 2 * bo;   // d0 in {-1,0,1}, d1 in {-2..1}
+        // vertex validity (geometry_np.py:628-639); R0 >= 0 and R0 < h always
+        const bool r1in = R1 < G.h;
+        const bool v1 = c0 >= 0 && c0 < G.w;
+        const bool v2 = flag ? (r1in && c1 >= 0 && c1 < G.w) : (c0 + 1 >= 0 && c0 + 1 < G.w);
+        const bool v3 = r1in && c1 + 1 >= 0 && c1 + 1 < G.w;
+        const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a * yrow));
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            // input rows R0-1 .. R0+2 = 2a-1+E .. 2a+2+E: ring slots (2K+E .. 2K+E+3) % 10
+            float xe[4], xo[4];
+            xrowf(PIC<(2 * K + E) % 10>{}, R0 - 1, c, xe[0], xo[0]);
+            xrowf(PIC<(2 * K + E + 1) % 10>{}, R0, c, xe[1], xo[1]);
+            xrowf(PIC<(2 * K + E + 2) % 10>{}, R0 + 1, c, xe[2], xo[2]);
+            xrowf(PIC<(2 * K + E + 3) % 10>{}, R0 + 2, c, xe[3], xo[3]);
+            float pe[4], ne[4], no[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pe[k] = ps_prev(xo[k]);                 // column ce - 1
+                ne[k] = ps_next(xe[k]);                 // column ce + 2
+                no[k] = OP == 0 ? ps_next(xo[k]) : 0.f; // column ce + 3
+            }
+            const float* w = &wk[c * 7];
+            // conv row R0 + q (parity (E + q) & 1) from input rows k = q + ii
+            auto conv = [&](auto Qc, float& ye, float& yo) {
+                constexpr int Q = decltype(Qc)::value, PAR = (E + Q) & 1;
+                ye = bv[c];
+                yo = bv[c];
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    const int k = Q + ps_tap_ii(t), s = ps_tap_shift(t, PAR, OP);
+                    const float ae = s == -1 ? pe[k] : (s == 0 ? xe[k] : (s == 1 ? xo[k] : ne[k]));
+                    const float ao = s == -1 ? xe[k] : (s == 0 ? xo[k] : (s == 1 ? ne[k] : no[k]));
+                    ye = fmaf(w[t], ae, ye);
+                    yo = fmaf(w[t], ao, yo);
+                }
+            };
+            float y0e, y0o, y1e, y1o;
+            conv(PIC<0>{}, y0e, y0o);
+            conv(PIC<1>{}, y1e, y1o);
+            // vertices: row R0 at columns 2b + d0 (+1), row R1 at 2b + d1 (+1)
+            const float y0pm = ps_prev(y0o), y0ne = ps_next(y0e);
+            const float y1pe = ps_prev(y1e), y1po = ps_prev(y1o), y1ne = ps_next(y1e);
+            const float p1 = d0 < 0 ? y0pm : (d0 == 0 ? y0e : y0o);
+            const float p2a = d0 < 0 ? y0e : (d0 == 0 ? y0o : y0ne);
+            const float p2b = d1 < -1 ? y1pe : (d1 == -1 ? y1po : (d1 == 0 ? y1e : y1o));
+            const float p3 = d1 < -1 ? y1po : (d1 == -1 ? y1e : (d1 == 0 ? y1o : y1ne));
+            const float q1 = v1 ? p1 : 0.f;
+            const float q2 = v2 ? (flag ? p2b : p2a) : 0.f;
+            const float q3 = v3 ? p3 : 0.f;
+            const float z = fmaf(wg, q3, fmaf(wb, q2, wa * q1));
+            __builtin_amdgcn_raw_buffer_store_b16(
+                __builtin_bit_cast(unsigned short, (Tout)z), yrs, yoff, so + c * yplane, 0);
+        }
+    };
+
+    // per-row lattice (uniform; fp64 on every lane)
+    auto row_lat = [&](int a, double& i_, int& i_n) {
+        i_ = axis_at(G.xs, a) + ch;
+        i_n = __builtin_amdgcn_readfirstlane((int)i_);
+    };
+    // step a (= a0 + K + 5m) with its prefetch of input rows 2a+6, 2a+7
+    auto full = [&](auto Kc, int a) {
+        constexpr int K = decltype(Kc)::value;
+        issue(PIC<(2 * K + 7) % 10>{}, 2 * a + 6);
+        issue(PIC<(2 * K + 8) % 10>{}, 2 * a + 7);
+        double i_;
+        int i_n;
+        row_lat(a, i_, i_n);
+        if (i_n == 2 * a) step(Kc, PIC<0>{}, a, i_, i_n);
+        else step(Kc, PIC<1>{}, a, i_, i_n);   // i_n = 2a + 1 (host-checked)
+    };
+
+    // prologue: input rows 2a0-1 .. 2a0+5
+    issue(PIC<0>{}, rb0);
+    issue(PIC<1>{}, rb0 + 1);
+    issue(PIC<2>{}, rb0 + 2);
+    issue(PIC<3>{}, rb0 + 3);
+    issue(PIC<4>{}, rb0 + 4);
+    issue(PIC<5>{}, rb0 + 5);
+    issue(PIC<6>{}, rb0 + 6);
+    int a = a0;
+    for (; a + 5 <= a1; a += 5) {
+        full(PIC<0>{}, a);
+        full(PIC<1>{}, a + 1);
+        full(PIC<2>{}, a + 2);
+        full(PIC<3>{}, a + 3);
+        full(PIC<4>{}, a + 4);
+    }
+    if (a < a1) {
+        full(PIC<0>{}, a);
+        if (a + 1 < a1) {
+            full(PIC<1>{}, a + 1);
+            if (a + 2 < a1) {
+                full(PIC<2>{}, a + 2);
+                if (a + 3 < a1) full(PIC<3>{}, a + 3);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+// The lattice class the kernel assumes, checked on the lattice itself (O(h1 + w1)):
+//   * i_n(a) - 2a in {0, 1} for every output row a;
+//   * c0 - 2b = floor(0.5 i_f(a) - 0.5 e(a) + g(b)) in {-1, 0, 1}, with
+//     g(b) = y_(b) + (w - 0.5)/2 - 2b: bounded by the extreme row and column terms plus
+//     a margin for the fp64 rounding of j_.
+static bool ps_lattice_ok(const Geom& g) {
+    double qmin = 1e300, qmax = -1e300, gmin = 1e300, gmax = -1e300;
+    const double ch = (double)(g.h - 1) * 0.5, cw = ((double)g.w - 0.5) * 0.5;
+    for (int64_t a = 0; a < g.h1; ++a) {
+        const double i_ = axis_at(g.xs, a) + ch;
+        const int64_t in = (int64_t)i_;
+        const int64_t e = in - 2 * a;
+        if (e < 0 || e > 1 || in < 0 || in >= g.h) return false;
+        const double q = 0.5 * (i_ - (double)in) - 0.5 * (double)e;
+        qmin = std::min(qmin, q);
+        qmax = std::max(qmax, q);
+    }
+    for (int64_t b = 0; b < g.w1; ++b) {
+        const double gb = axis_at(g.ys, b) + cw - 2.0 * (double)b;
+        gmin = std::min(gmin, gb);
+        gmax = std::max(gmax, gb);
+    }
+    // (j_ = a + 2b + q + g >= -eps: the kernel's trunc is the floor of this bound, or one
+    // more for a j_ rounded just below 0 at a = b = 0, where q + g = 0)
+    const double eps = 1e-6;
+    return qmin + gmin - eps >= -1.0 && qmax + gmax + eps < 2.0;
+}
+
+template <int OP, int C, typename Tin, typename Tout>
+static int ps_launch(const void* src, void* dst, const PyrStreamGeom& G, hipStream_t st) {
+    const int64_t blocks = G.B * (int64_t)G.nband * ((G.nwin + 3) / 4);
+    if (blocks > INT_MAX) return HG_ESHAPE;
+    hipLaunchKernelGGL((k_pyr_stream<OP, C, Tin, Tout>), dim3((unsigned)blocks), dim3(PS_THREADS),
+                       0, st, (const Tin*)src, (Tout*)dst, G);
+    return launch_status();
+}
+
+template <int OP, typename Tin, typename Tout>
+static int ps_channels(const void* src, void* dst, const PyrStreamGeom& G, int C, hipStream_t st) {
+    if (C == 3) return ps_launch<OP, 3, Tin, Tout>(src, dst, G, st);
+    if (C == 1) return ps_launch<OP, 1, Tin, Tout>(src, dst, G, st);
+    return HG_EUNSUP;
+}
+
+// One pyramid level on the streaming kernel, or HG_EUNSUP (the caller runs k_pyr_level).
+int pyr_stream_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
+                   int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
+                   const float* bias, int even_odd_offset, hipStream_t st) {
+    if (const char* e = getenv("HYGRID_PYRSTREAM")) {   // A/B switch for measurements
+        if (e[0] == '0') return HG_EUNSUP;
+    }
+    if (C != 1 && C != 3) return HG_EUNSUP;
+    if ((w & 1) || w < 2 || h < 2 || h1 < 1 || w1 < 1) return HG_EUNSUP;
+    if (src_dtype != dst_dtype || (src_dtype != HG_F16 && src_dtype != HG_BF16)) return HG_EUNSUP;
+    if (reinterpret_cast<uintptr_t>(src) & 3) return HG_EUNSUP;   // dword loads
+    if (C * h * w * 2 >= ((int64_t)1 << 31) || C * h1 * w1 * 2 >= ((int64_t)1 << 31))
+        return HG_EUNSUP;                                         // 32-bit buffer offsets
+    const Geom g = make_tri(h, w, h1, w1, 0.5);
+    if (!ps_lattice_ok(g)) return HG_EUNSUP;
+    PyrStreamGeom G;
+    G.B = batch;
+    G.h = (int)h; G.w = (int)w; G.h1 = (int)h1; G.w1 = (int)w1;
+    G.nwin = (int)((w1 + PS_OWN - 1) / PS_OWN);
+    G.nband = (int)((h1 + PS_RB - 1) / PS_RB);
+    G.xs = g.xs;
+    G.ys = g.ys;
+    G.taps = taps;
+    G.bias = bias;
+    const int op = (even_odd_offset + 1) & 1;   // tap column class at padding 1
+    if (src_dtype == HG_F16)
+        return op ? ps_channels<1, _Float16, _Float16>(src, dst, G, (int)C, st)
+                  : ps_channels<0, _Float16, _Float16>(src, dst, G, (int)C, st);
+    return op ? ps_channels<1, __bf16, __bf16>(src, dst, G, (int)C, st)
+              : ps_channels<0, __bf16, __bf16>(src, dst, G, (int)C, st);
+}
+
+}  // namespace hg

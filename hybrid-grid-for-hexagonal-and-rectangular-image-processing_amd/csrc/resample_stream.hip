@@ -37,13 +37,21 @@ namespace hg {
 
 constexpr int ST_THREADS = 256;     // 4 waves per workgroup: 4 adjacent windows
 constexpr int ST_COLS = 256;        // columns per window (4 per lane)
-constexpr int ST_RB = 128;          // rows per band (2 row records per lane)
+// Rows per band (<= 128: 2 row records per lane; even: h2r row parity is static).  Short
+// bands measured faster (more waves in flight over fewer rows of each image; in-process
+// A/B on 4K bf16 b128, tools/ab_ops.py: r2h 2.60 -> 2.49 ms at 24, h2r 2.55 -> 2.37 ms at 16).
+#ifndef ST_RB_R2H
+#define ST_RB_R2H 24
+#endif
+#ifndef ST_RB_H2R
+#define ST_RB_H2R 16
+#endif
 constexpr unsigned ST_OOB = 0x80000000u;   // buffer offset past num_records: loads 0, stores drop
 
 struct StreamGeom {
     int64_t planes;
     int h, w, h1, w1;
-    int nwin, nband;
+    int nwin, nband, rb;            // windows, bands, rows per band
     Axis rxs, rys;                  // r2h axes
     float tri[2][3];                // h2r (alpha, beta, gamma) for even / odd output rows
 };
@@ -136,8 +144,8 @@ __device__ __forceinline__ WaveUnit st_unit(const StreamGeom& S, int nrows) {
     const int band = (int)(rest % S.nband);
     u.plane = rest / S.nband;
     u.win = grp * 4 + wslot;
-    u.s0 = band * ST_RB;
-    u.s1 = min(u.s0 + ST_RB, nrows);
+    u.s0 = band * S.rb;
+    u.s1 = min(u.s0 + S.rb, nrows);
     u.live = u.plane < S.planes && u.win < S.nwin;
     return u;
 }
@@ -321,7 +329,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_h2r_stream(const Tin* __restrict
         }
         st_store4<Tout>(o, yrs, yoff, (unsigned)a * yrow);
     };
-    // bands start on even rows (ST_RB is even): four rows per trip, parity static,
+    // bands start on even rows (S.rb is even): four rows per trip, parity static,
     // every hex row loaded once
     StRow P;
     load_row(u.s0, P);
@@ -424,7 +432,8 @@ int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t pla
         if (!h2r_exact(g, S.tri)) return HG_EUNSUP;
     }
     S.nwin = (int)((w1 + ST_COLS - 1) / ST_COLS);
-    S.nband = (int)((h1 + ST_RB - 1) / ST_RB);
+    S.rb = op == HG_OP_RECT_TO_HEX ? ST_RB_R2H : ST_RB_H2R;
+    S.nband = (int)((h1 + S.rb - 1) / S.rb);
     if (sdt == HG_BF16 && ddt == HG_BF16) return stream_launch<__bf16, __bf16>(op, src, dst, S, st);
     if (sdt == HG_F16 && ddt == HG_F16) return stream_launch<_Float16, _Float16>(op, src, dst, S, st);
     if (sdt == HG_F32 && ddt == HG_F32) return stream_launch<float, float>(op, src, dst, S, st);

@@ -165,3 +165,39 @@ def test_pyramid_level_16bit_and_nan(dt):
     ulp = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
     scale = float(ref[fin].abs().max())
     torch.testing.assert_close(y.float()[fin], ref[fin], rtol=ulp, atol=ulp * scale)
+
+
+STREAM_CASES = [  # (B, C, h, w): 2x downsamples the row-streaming level kernel takes
+    (2, 3, 64, 130), (1, 1, 200, 250), (2, 3, 34, 500), (1, 3, 10, 8), (1, 3, 540, 960),
+    (1, 1, 122, 244),
+]
+
+
+@pytest.mark.parametrize("case", STREAM_CASES)
+@pytest.mark.parametrize("off", [0, 1])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_pyramid_level_stream_vs_oracle_and_lds(case, off, dt, monkeypatch):
+    """k_pyr_stream (pyramid_stream.hip: 16-bit, 2x downsample, bands of 30 output rows,
+    windows of 60 output columns) against the fp64 oracle chain within one output rounding
+    of the fp32 result, and against the LDS-tiled k_pyr_level (HYGRID_PYRSTREAM=0) within
+    one output rounding: ragged bands / windows, 1 and 3 channels, both tap classes, bias."""
+    B, C, h, w = case
+    h1, w1 = h // 2, w // 2
+    g = torch.Generator().manual_seed(h * 3 + w + off)
+    taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
+    bias = (torch.rand((C,), generator=g) - 0.5).to(DEV)
+    x = torch.rand((B, C, h, w), generator=g).to(DEV).to(dt)
+    y = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=False)
+    monkeypatch.setenv("HYGRID_PYRSTREAM", "0")
+    y_lds = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=False)
+    monkeypatch.delenv("HYGRID_PYRSTREAM")
+    assert y is not None and y_lds is not None and y.dtype == dt
+    xd = x.double().cpu().numpy()
+    c = O.hexconv2d(xd, taps.cpu().double().numpy(), bias.cpu().double().numpy(), off, 2,
+                    padding=1, groups=C)
+    ref = O.hexresize(c, (h1, w1), 1).reshape(B, C, h1, w1)
+    ulp = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
+    scale = float(np.abs(ref).max())
+    got = y.double().cpu().numpy()
+    np.testing.assert_allclose(got, ref, rtol=ulp, atol=ulp * scale)
+    torch.testing.assert_close(y.float(), y_lds.float(), rtol=2 * ulp, atol=2 * ulp * scale)

@@ -1,0 +1,103 @@
+"""Interleaved in-process A/B timing of library variants for the unfused hot-path operators
+(one process, same device buffers, HIP events on the launch stream; median / min per launch).
+
+usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
+  OP: r2h | h2r | conv | r2h32 | h2r32 | pyr   (bf16 4K b128 for r2h/h2r/conv; fp32 1080p b32
+      for r2h32/h2r32; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K)
+  name 'base' = the in-tree library; others = HyGrid/_lib/variants/libhygrid_<name>.so;
+  'name%VAR=VAL' runs that library with the environment variable VAR=VAL set around its calls
+  (the library's A/B switches, e.g. base%HYGRID_PYRSTREAM=0)
+"""
+import ctypes
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "hybrid-grid-for-hexagonal-and-rectangular-image-processing_amd",
+                      "HyGrid", "_lib")
+_i64, _int, _vp, _dbl = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_double
+
+
+def load(name):
+    name = name.split("%")[0]
+    path = os.path.join(LIBDIR, "libhygrid_hip.so") if name == "base" else \
+        os.path.join(LIBDIR, "variants", f"libhygrid_{name}.so")
+    return ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+
+
+def main():
+    op, rounds, names = sys.argv[1], int(sys.argv[2]), sys.argv[3:]
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream()
+    libs = {n: load(n) for n in names}
+    sys.path[:0] = [os.path.join(ROOT, "hybrid-grid-for-hexagonal-and-rectangular-image-processing_amd")]
+    from HyGrid import _abi
+    dt = {torch.bfloat16: _abi.HG_BF16, torch.float16: _abi.HG_F16, torch.float32: _abi.HG_F32}
+    g = torch.Generator(device=dev).manual_seed(2)
+    if op in ("r2h", "h2r", "conv"):
+        B, C, H, W, t = 128, 3, 2160, 3840, torch.bfloat16
+    elif op in ("r2h32", "h2r32"):
+        B, C, H, W, t = 32, 3, 1080, 1920, torch.float32
+    else:
+        B, C, H, W, t = 8, 3, 4320, 7680, torch.float16
+    x = torch.rand((B, C, H, W), generator=g, device=dev, dtype=t)
+    if op == "pyr":
+        y = torch.empty((B, C, H // 2, W // 2), device=dev, dtype=t)
+        taps = (torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32, device=dev) / 12).repeat(C)
+    else:
+        y = torch.empty_like(x)
+    k = (torch.rand((3, 21), generator=g, device=dev) - 0.5) * 0.5
+    b = torch.rand((3,), generator=g, device=dev) - 0.5
+    s = st.cuda_stream
+
+    def call(lib):
+        if op in ("r2h", "r2h32"):
+            f = lib.hg_rect_to_hex
+            f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_int, _vp]
+            return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, H, W, 1, s)
+        if op in ("h2r", "h2r32"):
+            f = lib.hg_hex_to_rect
+            f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_int, _vp]
+            return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, H, W, 1, s)
+        if op == "conv":
+            f = lib.hg_hexconv2d
+            f.argtypes = [_vp] * 4 + [_int] * 3 + [_i64] * 5 + [_int] * 7 + [_dbl, _vp]
+            return f(x.data_ptr(), k.data_ptr(), b.data_ptr(), y.data_ptr(), dt[t], _abi.HG_F32,
+                     dt[t], B, C, C, H, W, 2, 1, 1, 1, 1, 0, 0, 0.0, s)
+        f = lib.hg_hex_pyramid_level
+        f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 6 + [_vp, _vp, _int, _int, _vp]
+        return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B, C, H, W, H // 2, W // 2,
+                 taps.data_ptr(), None, 0, 0, s)
+
+    times = {n: [] for n in names}
+    sums = {}
+    for r in range(rounds + 1):
+        for n, lib in libs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            env = n.split("%")[1].split("=") if "%" in n else None
+            if env:
+                os.environ[env[0]] = env[1]
+            e0.record()
+            rc = call(lib)
+            e1.record()
+            if env:
+                del os.environ[env[0]]
+            if rc != 0:
+                raise SystemExit(f"{n}: status {rc}")
+            e1.synchronize()
+            if r > 0:
+                times[n].append(e0.elapsed_time(e1))
+            if r == rounds:
+                sums[n] = float(y.double().sum().item())
+    alg = x.numel() * x.element_size() + y.numel() * y.element_size()
+    for n in names:
+        tm = times[n]
+        print(f"{op:6s} {n:14s} median {statistics.median(tm):.4f} ms  min {min(tm):.4f} ms  "
+              f"{alg / statistics.median(tm) / 1e6:.0f} GB/s  checksum {sums[n]:.9e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -11,6 +11,7 @@ OUT=$PKG/HyGrid/_lib/variants
 mkdir -p "$OUT" "$OBJ/variants"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -DFU_MIN_INST=1 "$@" \
     -I"$PKG/csrc" -c "${FUSED_SRC:-$PKG/csrc/fused.hip}" -o "$OBJ/variants/fused_$NAME.o"
+# slim library: only what hg_pipeline_r2h_conv_h2r needs (tools/ab_fused.py calls nothing else)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libhygrid_$NAME.so" \
-    $(ls "$OBJ"/*.o | grep -v '/fused.o$') "$OBJ/variants/fused_$NAME.o"
+    "$OBJ/abi.o" "$OBJ/pipeline.o" "$OBJ/variants/fused_$NAME.o"
 echo "$OUT/libhygrid_$NAME.so"
