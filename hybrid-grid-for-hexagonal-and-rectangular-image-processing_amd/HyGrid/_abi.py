@@ -80,6 +80,7 @@ SIGNATURES = {
                                + [_i64, _i64, _vp], _int),
     "hg_hex_pyramid_level": ([_vp, _vp, _int, _int] + [_i64] * 6 + [_vp, _vp, _int, _int, _vp],
                              _int),
+    "hg_pipeline_r2h_h2r": ([_vp, _vp, _int, _int] + [_i64] * 5 + [_vp], _int),
     "hg_pipeline_r2h_conv_h2r": ([_vp, _vp, _vp, _vp, _int, _int] + [_i64] * 9 +
                                  [_int, _int, _int, _dbl, _vp], _int),
 }

@@ -439,6 +439,31 @@ def strided_copy2d(x, row_start, row_step, col_start, col_step, h_out=None, w_ou
 HG_EUNSUP = -4
 
 
+def pipeline_r2h_h2r(x, hex_size=None, out_dtype=None):
+    """Fused rect -> hex (bilinear) -> rect (linear) round trip, no conv: the same result as
+    hex_to_rect(rect_to_hex(x, hex_size), hex_size) (geometry_np.py:358-519, :191-356) with
+    the hex image kept in fp32 on chip.  x: (..., h, w) device tensor -> (..., h1, w1).
+
+    Returns None when the fused kernel does not cover the geometry / dtypes (the caller then
+    runs the two resamplers); raises on argument errors.
+    """
+    _abi.require_device(x)
+    x = x.contiguous()
+    h, w = int(x.shape[-2]), int(x.shape[-1])
+    planes = x.numel() // max(h * w, 1)
+    h1, w1 = (h, w) if hex_size is None else (int(hex_size[0]), int(hex_size[1]))
+    if out_dtype is None:
+        out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
+    y = torch.empty(tuple(x.shape[:-2]) + (h1, w1), dtype=out_dtype, device=x.device)
+    st = _abi.lib().hg_pipeline_r2h_h2r(_abi.ptr(x), _abi.ptr(y), _abi.dtype_code(x.dtype),
+                                        _abi.dtype_code(out_dtype), planes, h, w, h1, w1,
+                                        _abi.stream_of(x))
+    if st in (HG_EUNSUP, -2):
+        return None
+    _abi.check(st, "hg_pipeline_r2h_h2r")
+    return y
+
+
 def pipeline_r2h_conv_h2r(x, kernel, bias, hex_size=None, rect_size=None, padding=1, groups=1,
                           even_odd_offset=0, padding_value=0.0, out_dtype=None):
     """Fused rect -> hex (bilinear) -> HexConv2d (radius 2) -> hex -> rect (linear).

@@ -13,7 +13,7 @@ import torch
 from . import ops
 from .HexFrames import HexConv2d
 
-__all__ = ["rect_hex_conv_rect", "fusable", "hex_pyramid", "pyramid_fusable"]
+__all__ = ["rect_hex_conv_rect", "rect_hex_rect", "fusable", "hex_pyramid", "pyramid_fusable"]
 
 
 def fusable(conv):
@@ -42,6 +42,22 @@ def rect_hex_conv_rect(x, conv, hex_size=None, rect_size=None, out_dtype=None, f
     h = ops.rect_to_hex(x, hex_size, out_dtype=torch.float32)
     c = conv(h)
     return ops.hex_to_rect(c, rect_size, out_dtype=out_dtype)
+
+
+def rect_hex_rect(x, hex_size=None, out_dtype=None, fused=True):
+    """The rect -> hex -> rect round trip (BASELINE config 2): x (..., H, W) device tensor ->
+    (..., h1, w1), the same result as ops.hex_to_rect(ops.rect_to_hex(x, hex_size), hex_size)
+    (geometry_np.py:358-519 then :191-356) with the hex image in fp32.  One pass of the
+    fused kernel (hg_pipeline_r2h_h2r) for the same-size lattices, else the two resamplers.
+    """
+    if out_dtype is None:
+        out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
+    if fused:
+        y = ops.pipeline_r2h_h2r(x, hex_size, out_dtype)
+        if y is not None:
+            return y
+    h = ops.rect_to_hex(x, hex_size, out_dtype=torch.float32)
+    return ops.hex_to_rect(h, tuple(h.shape[-2:]), out_dtype=out_dtype)
 
 
 def pyramid_fusable(conv):

@@ -14,6 +14,11 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
               int64_t h1, int64_t w1, int64_t h2, int64_t w2, int padding, int op,
               double pad_value, hipStream_t st);
 
+// rect -> hex -> rect round trip (no conv) on the same kernel, same-size lattices, even
+// widths, planes of (h, w) -> (h1, w1); HG_EUNSUP otherwise.
+int fused_rt_try(const void* x, void* y, int x_dtype, int y_dtype, int64_t planes, int64_t h,
+                 int64_t w, int64_t h1, int64_t w1, hipStream_t st);
+
 // HexConv2d alone on the same kernel (fused_conv.hip): radius 2, stride 1, padding 1,
 // pad value 0, no epilogue, C/O/groups as above, even widths; HG_EUNSUP otherwise.
 int fused_conv_try(const void* x, const float* kernel, const float* bias, void* y, int x_dtype,

@@ -82,6 +82,43 @@ static bool fused_geometry_ok(const Geom& g) {
     return true;
 }
 
+// Round trip rect -> hex -> rect without the conv (MD 2), one plane per "image" (C = 1):
+// geometry_np.hex_to_rect_resample(rect_to_hex_resample(x, (h1, w1)), (h1, w1)) with the hex
+// image kept on chip in fp32.
+int fused_rt_try(const void* x, void* y, int x_dtype, int y_dtype, int64_t planes, int64_t h,
+                 int64_t w, int64_t h1, int64_t w1, hipStream_t st) {
+    if (const char* e = getenv("HYGRID_FUSED2")) {   // A/B switch for measurements
+        if (e[0] == '0') return HG_EUNSUP;
+    }
+    if ((w & 1) || (w1 & 1) || w < 2 || h1 < 1 || planes < 1) return HG_EUNSUP;
+    if (x_dtype != HG_BF16 && x_dtype != HG_F16 && x_dtype != HG_F32) return HG_EUNSUP;
+    if (y_dtype != HG_BF16 && y_dtype != HG_F16 && y_dtype != HG_F32) return HG_EUNSUP;
+    if (h * w * 8 >= ((int64_t)1 << 31) || h1 * w1 * 4 >= ((int64_t)1 << 31)) return HG_EUNSUP;
+    const Geom g = make_r2h(h, w, h1, w1);
+    if (!fused_geometry_ok(g)) return HG_EUNSUP;
+    FusedGeom F;
+    F.B = planes;
+    F.h = (int)h; F.w = (int)w; F.h1 = (int)h1; F.w1 = (int)w1; F.h2 = (int)h1; F.w2 = (int)w1;
+    F.rxs = g.xs;
+    F.rys = g.ys;
+    F.nwin = (int)((w1 + FU_OWN - 1) / FU_OWN);
+    F.nband = (int)((h1 + FU_RB - 1) / FU_RB);
+    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + 3) / 4);
+    if (blocks > INT_MAX) return HG_ESHAPE;
+    const dim3 grid((unsigned)blocks), blk(FU_THREADS);
+#define HG_RT(TI, TO)                                                                          \
+    hipLaunchKernelGGL((k_fused<TI, TO, 1, 1, 1, 0, 2>), grid, blk, 0, st, (const TI*)x,        \
+                       (const float*)nullptr, (const float*)nullptr, (TO*)y, F);               \
+    return launch_status();
+    if (x_dtype == HG_F32 && y_dtype == HG_F32) { HG_RT(float, float) }
+    if (x_dtype == HG_BF16 && y_dtype == HG_BF16) { HG_RT(__bf16, __bf16) }
+    if (x_dtype == HG_F16 && y_dtype == HG_F16) { HG_RT(_Float16, _Float16) }
+    if (x_dtype == HG_BF16 && y_dtype == HG_F32) { HG_RT(__bf16, float) }
+    if (x_dtype == HG_F16 && y_dtype == HG_F32) { HG_RT(_Float16, float) }
+#undef HG_RT
+    return HG_EUNSUP;
+}
+
 int fused_try(const void* x, const float* kernel, const float* bias, void* y, int x_dtype,
               int y_dtype, int64_t batch, int C, int O, int G, int64_t h, int64_t w,
               int64_t h1, int64_t w1, int64_t h2, int64_t w2, int padding, int op,

@@ -153,7 +153,9 @@ __host__ __device__ constexpr int fu_mod(int a, int m) { return ((a % m) + m) % 
 
 // MD 0: rect -> hex -> HexConv2d -> hex -> rect (the pipeline).  MD 1: HexConv2d alone
 // (radius 2, stride 1, padding 1, pad value 0; HexFrames.py:96-169): the "u rows" are
-// the input hex rows themselves and conv rows are stored as they complete.
+// the input hex rows themselves and conv rows are stored as they complete.  MD 2: the
+// round trip rect -> hex -> rect without the conv (BASELINE config 2): each u row is its
+// own "conv row" (C == O, no weights) and goes straight through the h2r filter.
 template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD = 0>
 // MD 1 with 16-bit input and output fits 128 VGPRs (4 waves per SIMD); an fp32 raw ring or
 // fp32 stores need more, and capping those at 128 spills to scratch inside the row loop.
@@ -218,7 +220,7 @@ void k_fused(const Tin* __restrict__ x,
     // (table c == 0), RC 2 if rows r, r+1 (a == 0): two terms per vertical blend instead
     // of three.  A same-size lattice switches class once, in the middle band.
     int rc = 0;
-    if (MD == 0 && FU_RC) {
+    if (MD != 1 && FU_RC) {
         bool has_a = false, has_c = false;
         for (int e = lane; e < NLUT; e += 64) {
             const float4 t = lut[e];
@@ -234,7 +236,7 @@ void k_fused(const Tin* __restrict__ x,
     // r2h (geometry_np.py:441-449, 514-517): u[q] = sum_k wr_k[q] v[q+k], k = -1..1
     float we[3] = {0.f, 0.f, 0.f}, wo_[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 2 && MD == 0; ++s) {
+    for (int s = 0; s < 2 && MD != 1; ++s) {
         const int q = ce + s;
         float* wr = s ? wo_ : we;
         if (q >= 0 && q < F.w1) {
@@ -294,10 +296,10 @@ void k_fused(const Tin* __restrict__ x,
     const float ws_ = FOLD ? 0.75f : 1.f;
     float wk[O * CG * 7];
 #pragma unroll
-    for (int i = 0; i < O * CG * 7; ++i) wk[i] = kern[i + (FU_WSGPR ? 0 : vz)] * ws_;
+    for (int i = 0; i < O * CG * 7; ++i) wk[i] = MD == 2 ? 0.f : kern[i + (FU_WSGPR ? 0 : vz)] * ws_;
     float bv[O];
 #pragma unroll
-    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] * ws_ : 0.f;
+    for (int o = 0; o < O; ++o) bv[o] = (MD != 2 && bias) ? bias[o + vz] * ws_ : 0.f;
     float c75 = 0.75f, c25 = 0.25f;     // h2r weights as VGPR operands, not literals
     float c13 = 1.f / 3.f;
     asm volatile("" : "+v"(c75), "+v"(c25), "+v"(c13));
@@ -375,6 +377,14 @@ void k_fused(const Tin* __restrict__ x,
                     ue[c] = fmaf(we[2], vo, fmaf(we[1], ve, we[0] * vpo));
                     uo[c] = fmaf(wo_[2], vne, fmaf(wo_[1], vo, wo_[0] * ve));
                 }
+            }
+            if constexpr (MD == 2) {                // z row r = u row r (no conv)
+    #pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    ZE[S1][c] = ue[c];
+                    ZO[S1][c] = uo[c];
+                }
+                return;
             }
     #pragma unroll
             for (int c = 0; c < C; ++c) {

@@ -952,3 +952,19 @@ extern "C" int hg_pipeline_r2h_conv_h2r(const void* x, const float* kernel, cons
         return HG_EDTYPE;
     }
 }
+
+// rect -> hex -> rect round trip without a conv (BASELINE config 2) in one pass: replaces
+// geometry_np.hex_to_rect_resample(geometry_np.rect_to_hex_resample(x, (h1, w1)), (h1, w1))
+// (geometry_np.py:358-519 then :191-356, 'bilinear' / 'linear') for the same-size lattices
+// (fused.hip, MD 2); HG_EUNSUP elsewhere (run the two resamplers instead).
+extern "C" int hg_pipeline_r2h_h2r(const void* x, void* y, int x_dtype, int y_dtype,
+                                   int64_t planes, int64_t h, int64_t w, int64_t h1, int64_t w1,
+                                   void* stream) {
+    using namespace hg;
+    if (planes < 0 || h < 1 || w < 1 || h1 < 1 || w1 < 1) return HG_EINVAL;
+    if (h > INT_MAX / 4 || w > INT_MAX / 4 || h1 > INT_MAX / 4 || w1 > INT_MAX / 4) return HG_ESHAPE;
+    if (planes == 0) return HG_OK;
+    if (!x || !y) return HG_EINVAL;
+    return fused_rt_try(x, y, x_dtype, y_dtype, planes, h, w, h1, w1,
+                        reinterpret_cast<hipStream_t>(stream));
+}

@@ -4,8 +4,9 @@
 //
 // The general kernels (resample.hip) stage a 2-D footprint per (tile, plane) in LDS.
 // When the lattice is a near identity every output sample's taps sit in the same or
-// the neighbouring row and column, so a wavefront can own a 256-column window of one
-// plane (4 columns per lane, 8/16-byte loads and stores) and walk a band of rows:
+// the neighbouring row and column, so a wavefront can own a window of one plane (4
+// columns per lane for 16-bit data, 2 when either side is fp32: 4- or 8-byte loads and
+// stores per lane) and walk a band of rows:
 //
 //  * r2h (geometry_np.py:440-517): output row r blends source rows in(r), in(r)+1 with
 //    in(r) - r in {-1, 0} (per-row record from the fp64 lattice, one row per lane,
@@ -36,7 +37,11 @@
 namespace hg {
 
 constexpr int ST_THREADS = 256;     // 4 waves per workgroup: 4 adjacent windows
-constexpr int ST_COLS = 256;        // columns per window (4 per lane)
+// Columns per lane: 4 when both sides are 16-bit (8-B loads and stores), 2 when either is
+// fp32 (8-B fp32 loads: 16-B-per-lane rows walked by a wave measured 22 % slower than 8-B
+// ones, tools/microbench/walk.hip, profiles/r02/probe/walk.txt).  Window = 64 lanes.
+template <typename Tin, typename Tout>
+constexpr int st_cpl() { return (sizeof(Tin) == 4 || sizeof(Tout) == 4) ? 2 : 4; }
 // Rows per band (<= 128: 2 row records per lane; even: h2r row parity is static).  Short
 // bands measured faster (more waves in flight over fewer rows of each image; in-process
 // A/B on 4K bf16 b128, tools/ab_ops.py: r2h 2.60 -> 2.49 ms at 24, h2r 2.55 -> 2.37 ms at 16).
@@ -64,17 +69,22 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t st_rsrc(const void* base, int6
                                              0x00020000);
 }
 
-// four consecutive elements (one lane's columns) as f32
-template <typename T>
-__device__ __forceinline__ void st_load4(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff,
-                                         float* v) {
-    if constexpr (sizeof(T) == 2) {
+// CPL consecutive elements (one lane's columns) as f32
+template <typename T, int CPL>
+__device__ __forceinline__ void st_load(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff,
+                                        float* v) {
+    if constexpr (sizeof(T) == 2 && CPL == 4) {
         const typename Vec4Of<T>::type r = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
         typedef T t4 __attribute__((ext_vector_type(4)));
         const t4 e = __builtin_bit_cast(t4, r);
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = (float)e[k];
-    } else {
+    } else if constexpr (sizeof(T) == 2) {
+        typedef T t2 __attribute__((ext_vector_type(2)));
+        const t2 e = __builtin_bit_cast(t2, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+        v[0] = (float)e[0];
+        v[1] = (float)e[1];
+    } else if constexpr (CPL == 4) {
         // whole-vector bit_cast: extracting lanes of the integer vector and casting each
         // (bit_cast(float, r[k])) is miscompiled by this toolchain's demanded-elements
         // narrowing of buffer loads (every element read as element 0)
@@ -82,6 +92,11 @@ __device__ __forceinline__ void st_load4(__amdgpu_buffer_rsrc_t rs, unsigned vof
         const f4 e = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
 #pragma unroll
         for (int k = 0; k < 4; ++k) v[k] = e[k];
+    } else {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 e = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+        v[0] = e[0];
+        v[1] = e[1];
     }
 }
 // one dword holding the element at the window edge: lo / hi half for 16-bit types
@@ -96,19 +111,28 @@ __device__ __forceinline__ void st_load_edge(__amdgpu_buffer_rsrc_t rs, unsigned
         *lo = *hi = __builtin_bit_cast(float, r);
     }
 }
-template <typename T>
-__device__ __forceinline__ void st_store4(const float* v, __amdgpu_buffer_rsrc_t rs, unsigned voff,
-                                          unsigned soff) {
-    if constexpr (sizeof(T) == 2) {
+template <typename T, int CPL>
+__device__ __forceinline__ void st_store(const float* v, __amdgpu_buffer_rsrc_t rs, unsigned voff,
+                                         unsigned soff) {
+    if constexpr (sizeof(T) == 2 && CPL == 4) {
         typedef T t4 __attribute__((ext_vector_type(4)));
         const t4 e = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(typename Vec4Of<T>::type, e), rs,
                                               voff, soff, 0);
-    } else {
+    } else if constexpr (sizeof(T) == 2) {
+        typedef T t2 __attribute__((ext_vector_type(2)));
+        const t2 e = {(T)v[0], (T)v[1]};
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, e), rs, voff, soff, 0);
+    } else if constexpr (CPL == 4) {
         typedef float f4 __attribute__((ext_vector_type(4)));
         const f4 e = {v[0], v[1], v[2], v[3]};
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(typename Vec4Of<T>::type, e), rs,
                                                voff, soff, 0);
+    } else {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        const f2 e = {v[0], v[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, e), rs, voff, soff, 0);
     }
 }
 
@@ -122,10 +146,15 @@ __device__ __forceinline__ float st_next(float v, float old) {
         __builtin_bit_cast(int, old), __builtin_bit_cast(int, v), 0x130 /*wave_shl:1*/, 0xf, 0xf, false));
 }
 
-// one source row as seen by a lane: its 4 columns and the window-edge dword halves
+// one source row as seen by a lane: its CPL columns and the window-edge dword halves
+template <int CPL>
 struct StRow {
-    float v[4], el, eh;
-    __device__ __forceinline__ void zero() { v[0] = v[1] = v[2] = v[3] = el = eh = 0.f; }
+    float v[CPL], el, eh;
+    __device__ __forceinline__ void zero() {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) v[k] = 0.f;
+        el = eh = 0.f;
+    }
 };
 
 struct WaveUnit {
@@ -153,14 +182,16 @@ __device__ __forceinline__ WaveUnit st_unit(const StreamGeom& S, int nrows) {
 // ---------------------------------------------------------------------------
 // rect -> hex, bilinear (geometry_np.py:358-519)
 // ---------------------------------------------------------------------------
-template <typename Tin, typename Tout>
+template <typename Tin, typename Tout, int CPL = st_cpl<Tin, Tout>()>
 __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict__ x,
                                                            Tout* __restrict__ y, StreamGeom S) {
     const WaveUnit u = st_unit(S, S.h1);
     if (!u.live) return;                          // wave-uniform; no barriers below
     const int lane = threadIdx.x & 63;
+    constexpr int ST_COLS = 64 * CPL;             // window columns
+    using StRow = hg::StRow<CPL>;
     const int W0 = u.win * ST_COLS;
-    const int ce = W0 + 4 * lane;                 // this lane's first column
+    const int ce = W0 + CPL * lane;               // this lane's first column
 
     // per-row records, row s0 + 64 k + lane (fp64 lattice, geometry_np.py:440-449)
     int rin[2];
@@ -183,10 +214,10 @@ __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict
     // per-column records (constant over rows): jn - q in {-1, 0}, fj, 1 - fj
     // (a column with no tap inside the raster, e.g. q = w1 - 1 where jn = w, is "dead":
     // both taps read 0 as in the general kernel)
-    float fj[4], gj[4];
-    bool left[4], dead[4];                        // jn == q - 1; no live tap
+    float fj[CPL], gj[CPL];
+    bool left[CPL], dead[CPL];                        // jn == q - 1; no live tap
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < CPL; ++k) {
         const int q = ce + k;
         fj[k] = 0.f; gj[k] = 0.f; left[k] = false; dead[k] = true;
         if (q < S.w1) {
@@ -203,11 +234,11 @@ __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict
     const int64_t ipl = (int64_t)S.h * S.w, opl = (int64_t)S.h1 * S.w1;
     const __amdgpu_buffer_rsrc_t xrs = st_rsrc(x + u.plane * ipl, ipl * (int64_t)sizeof(Tin));
     const __amdgpu_buffer_rsrc_t yrs = st_rsrc(y + u.plane * opl, opl * (int64_t)sizeof(Tout));
-    // lanes whose 4 columns are outside the raster read zeros (w % 4 == 0: all or none)
+    // lanes whose columns are outside the raster read zeros (w % CPL == 0: all or none)
     const unsigned xoff = ce < S.w ? (unsigned)ce * (unsigned)sizeof(Tin) : ST_OOB;
     const unsigned yoff = ce < S.w1 ? (unsigned)ce * (unsigned)sizeof(Tout) : ST_OOB;
     // edge dword: lane 0 -> column W0-1 (16-bit: dword W0-2..W0-1, hi half), lane 63 ->
-    // column W0+256 (lo half); zero outside the raster, no access for other lanes
+    // column W0+64*CPL (lo half); zero outside the raster, no access for other lanes
     constexpr int EB = sizeof(Tin) == 2 ? 2 : 1;
     unsigned eoff = ST_OOB;
     if (lane == 0 && W0 > 0) eoff = (unsigned)(W0 - EB) * (unsigned)sizeof(Tin);
@@ -220,7 +251,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict
     // in(r) - r in {-1, 0} need no further masking.
     auto load_row = [&](int rr, StRow& R) {
         const unsigned so = (unsigned)min(max(rr, 0), S.h - 1) * xrow;
-        st_load4<Tin>(xrs, xoff, so, R.v);
+        st_load<Tin, CPL>(xrs, xoff, so, R.v);
         st_load_edge<Tin>(xrs, eoff, so, &R.el, &R.eh);
         if (rr < 0 || rr >= S.h) R.zero();            // uniform
     };
@@ -239,23 +270,23 @@ __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict
         if (!(val & 1u)) A.zero();                    // a dead row (no live tap): all zero
         if (!(val & 2u)) B.zero();
         // vertical blend per column, t = c0 * P(in+1) + c1 * P(in)   (:515-516)
-        float t[4];
+        float t[CPL];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) t[c] = c0 * B.v[c] + c1 * A.v[c];
+        for (int c = 0; c < CPL; ++c) t[c] = c0 * B.v[c] + c1 * A.v[c];
         const float tl = c0 * B.eh + c1 * A.eh;       // column W0-1 (meaningful on lane 0)
-        const float tr = c0 * B.el + c1 * A.el;       // column W0+256 (lane 63)
-        const float tm = st_prev(t[3], tl);           // column ce - 1
-        const float tp = st_next(t[0], tr);           // column ce + 4
-        float o[4];
+        const float tr = c0 * B.el + c1 * A.el;       // column W0+64*CPL (lane 63)
+        const float tm = st_prev(t[CPL - 1], tl);           // column ce - 1
+        const float tp = st_next(t[0], tr);           // column ce + CPL
+        float o[CPL];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < CPL; ++c) {
             const float tc_m = c == 0 ? tm : t[c - 1];
-            const float tc_p = c == 3 ? tp : t[c + 1];
+            const float tc_p = c == CPL - 1 ? tp : t[c + 1];
             const float t1 = dead[c] ? 0.f : (left[c] ? tc_m : t[c]);   // column jn
             const float t2 = dead[c] ? 0.f : (left[c] ? t[c] : tc_p);   // column jn + 1
             o[c] = fj[c] * t2 + gj[c] * t1;           // :517
         }
-        st_store4<Tout>(o, yrs, yoff, (unsigned)r * yrow);
+        st_store<Tout, CPL>(o, yrs, yoff, (unsigned)r * yrow);
     };
     // four output rows per trip: four new source rows (r0+1 .. r0+4) issue together;
     // readlane is convergent, so the compiler would not unroll this loop by itself
@@ -280,14 +311,16 @@ __global__ __launch_bounds__(ST_THREADS) void k_r2h_stream(const Tin* __restrict
 // ---------------------------------------------------------------------------
 // hex -> rect, linear, same size (geometry_np.py:191-356)
 // ---------------------------------------------------------------------------
-template <typename Tin, typename Tout>
+template <typename Tin, typename Tout, int CPL = st_cpl<Tin, Tout>()>
 __global__ __launch_bounds__(ST_THREADS) void k_h2r_stream(const Tin* __restrict__ x,
                                                            Tout* __restrict__ y, StreamGeom S) {
     const WaveUnit u = st_unit(S, S.h1);
     if (!u.live) return;
     const int lane = threadIdx.x & 63;
+    constexpr int ST_COLS = 64 * CPL;             // window columns
+    using StRow = hg::StRow<CPL>;
     const int W0 = u.win * ST_COLS;
-    const int ce = W0 + 4 * lane;
+    const int ce = W0 + CPL * lane;
     const int64_t pl = (int64_t)S.h * S.w;        // h1 == h, w1 == w
     const __amdgpu_buffer_rsrc_t xrs = st_rsrc(x + u.plane * pl, pl * (int64_t)sizeof(Tin));
     const __amdgpu_buffer_rsrc_t yrs = st_rsrc(y + u.plane * pl, pl * (int64_t)sizeof(Tout));
@@ -302,7 +335,7 @@ __global__ __launch_bounds__(ST_THREADS) void k_h2r_stream(const Tin* __restrict
 
     auto load_row = [&](int rr, StRow& R) {       // ring row; zeros outside the raster
         const unsigned so = (unsigned)min(rr, S.h - 1) * xrow;
-        st_load4<Tin>(xrs, xoff, so, R.v);
+        st_load<Tin, CPL>(xrs, xoff, so, R.v);
         st_load_edge<Tin>(xrs, eoff, so, &R.el, &R.eh);
         if (rr >= S.h) R.zero();                      // uniform
     };
@@ -311,23 +344,23 @@ __global__ __launch_bounds__(ST_THREADS) void k_h2r_stream(const Tin* __restrict
         constexpr bool odd = decltype(ODDc)::value;
         if (a >= u.s1) return;                        // uniform (last trip of a band)
         const float al = S.tri[odd][0], be = S.tri[odd][1], ga = S.tri[odd][2];
-        float o[4];
+        float o[CPL];
         if constexpr (!odd) {                         // p1 = (a, b), p2 = (a, b+1)
-            const float zp = st_next(Z.v[0], Z.el);   // column ce + 4
+            const float zp = st_next(Z.v[0], Z.el);   // column ce + CPL
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float p2 = c == 3 ? zp : Z.v[c + 1];
+            for (int c = 0; c < CPL; ++c) {
+                const float p2 = c == CPL - 1 ? zp : Z.v[c + 1];
                 o[c] = al * Z.v[c] + be * p2 + ga * N.v[c];   // :354
             }
         } else {                                      // p1 = (a, b-1), p2 = (a, b)
-            const float zm = st_prev(Z.v[3], Z.eh);   // column ce - 1
+            const float zm = st_prev(Z.v[CPL - 1], Z.eh);   // column ce - 1
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
+            for (int c = 0; c < CPL; ++c) {
                 const float p1 = c == 0 ? zm : Z.v[c - 1];
                 o[c] = al * p1 + be * Z.v[c] + ga * N.v[c];
             }
         }
-        st_store4<Tout>(o, yrs, yoff, (unsigned)a * yrow);
+        st_store<Tout, CPL>(o, yrs, yoff, (unsigned)a * yrow);
     };
     // bands start on even rows (S.rb is even): four rows per trip, parity static,
     // every hex row loaded once
@@ -417,7 +450,8 @@ int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t pla
     auto small = [](int dt) { return dt == HG_BF16 || dt == HG_F16 || dt == HG_F32; };
     if (!small(sdt) || !small(ddt)) return HG_EUNSUP;   // f32 accumulator types only
     if (planes <= 0 || h < 2 || w < 4 || h1 < 1 || w1 < 4) return HG_EUNSUP;
-    if ((w & 3) || (w1 & 3)) return HG_EUNSUP;           // a lane's 4 columns: all in or out
+    const int cpl = (sdt == HG_F32 || ddt == HG_F32) ? 2 : 4;   // = st_cpl<Tin, Tout>()
+    if ((w % cpl) || (w1 % cpl)) return HG_EUNSUP;       // a lane's columns: all in or out
     if (h * w * 4 >= ((int64_t)1 << 31) || h1 * w1 * 4 >= ((int64_t)1 << 31)) return HG_EUNSUP;
     StreamGeom S = {};
     S.planes = planes;
@@ -431,7 +465,7 @@ int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t pla
         const Geom g = make_tri(h, w, h1, w1, 0.75);
         if (!h2r_exact(g, S.tri)) return HG_EUNSUP;
     }
-    S.nwin = (int)((w1 + ST_COLS - 1) / ST_COLS);
+    S.nwin = (int)((w1 + 64 * cpl - 1) / (64 * cpl));
     S.rb = op == HG_OP_RECT_TO_HEX ? ST_RB_R2H : ST_RB_H2R;
     S.nband = (int)((h1 + S.rb - 1) / S.rb);
     if (sdt == HG_BF16 && ddt == HG_BF16) return stream_launch<__bf16, __bf16>(op, src, dst, S, st);

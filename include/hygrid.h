@@ -219,6 +219,15 @@ int hg_pipeline_r2h_conv_h2r(const void* x, const float* kernel, const float* bi
                              int64_t h2, int64_t w2, int padding, int groups,
                              int even_odd_offset, double pad_value, void* stream);
 
+/* rect -> hex -> rect round trip (BASELINE config 2) in one pass, no conv: replaces
+ * hex_to_rect_resample(rect_to_hex_resample(x, (h1, w1), 'bilinear'), (h1, w1), 'linear')
+ * (HyGrid/geometry_np.py:358-519, then :191-356).  x: (planes, h, w); y: (planes, h1, w1);
+ * the hex image stays on chip in fp32.  x_dtype in {F16, BF16, F32}, y_dtype in {x_dtype,
+ * F32}.  Returns HG_EUNSUP unless the lattice is the same-size near-identity one and the
+ * widths are even (then run hg_rect_to_hex + hg_hex_to_rect). */
+int hg_pipeline_r2h_h2r(const void* x, void* y, int x_dtype, int y_dtype, int64_t planes,
+                        int64_t h, int64_t w, int64_t h1, int64_t w1, void* stream);
+
 /* One level of a hex Gaussian pyramid (BASELINE config 5) in one pass:
  *   from_rect = 0:  y = hexresize(HexConv2d_dw(x), (h1, w1))
  *   from_rect = 1:  y = hexresize(HexConv2d_dw(rect_to_hex(x, (h, w), 'bilinear')), (h1, w1))
