@@ -1,10 +1,8 @@
 #!/bin/bash
-# One GPU call: stream-kernel parity tests + op timings (tools/ab_ops.py) -> gpurun_out/$1/
+# One GPU call: op A/Bs of variant libraries (tools/ab_ops.py) -> gpurun_out/$1/ab.txt
 set -o pipefail
 TAG=${1:-ab}; mkdir -p gpurun_out/$TAG; O=gpurun_out/$TAG/ab.txt; : > $O
 export TMPDIR=/tmp
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_stream.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread \
-    > gpurun_out/$TAG/pytest.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/$TAG/pytest.log; exit 1; }
-tail -2 gpurun_out/$TAG/pytest.log
-for op in r2h32 h2r32 r2h h2r; do timeout -k 10 200 python3 -u tools/ab_ops.py $op 15 base >> $O 2>&1 || { cat $O; exit 1; }; done
+timeout -k 10 200 python3 -u tools/ab_ops.py pyr 15 base ps15 ps45 ps60 >> $O 2>&1 || { cat $O; exit 1; }
+timeout -k 10 200 python3 -u tools/ab_ops.py r2h 15 base >> $O 2>&1 || { cat $O; exit 1; }
 cat $O
