@@ -87,6 +87,25 @@ def test_fused_4k_bf16_matches_oracle_and_unfused():
     close(unf.cpu().numpy(), y32.cpu().numpy().astype(np.float64), 1e-5)
 
 
+def test_fused_config3_full_batch_sampled_images():
+    """The bench's own launch (BASELINE config 3: 128 x 3 x 2160 x 3840 bf16, bench.py's
+    seeds) in one call; three images across the batch (first, middle, last) against the
+    fp64 oracle chain at 1e-5 (fp32 output) and the bf16 output within one rounding."""
+    torch.manual_seed(3)
+    conv = HexConv2d(3, 3, 0, 2, padding=1, groups=1, bias=True).to(DEV)
+    gen = torch.Generator(device=DEV).manual_seed(2)
+    x = torch.rand((128, 3, 2160, 3840), generator=gen, device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        y32 = rect_hex_conv_rect(x, conv, out_dtype=torch.float32)
+        y = rect_hex_conv_rect(x, conv)
+    for i in (0, 63, 127):
+        ref = oracle_chain(x[i:i + 1], conv, (2160, 3840), (2160, 3840))[0]
+        close(y32[i].cpu().numpy(), ref, 1e-5)
+        close(y[i].float().cpu().numpy(), ref, 2 ** -8)
+    del x, y, y32
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("dt_in,dt_out", [
     (torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
     (torch.float16, torch.float16), (torch.float16, torch.float32),

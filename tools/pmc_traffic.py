@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGES = {   # json key -> (prof_pipeline stage, kernel-name substring)
     "pipeline_r2h_conv_h2r": ("fused", "k_fused"),
     "rect_to_hex": ("r2h", "k_r2h_stream"),
-    "hexconv2d": ("conv", "k_hexconv"),
+    "hexconv2d": ("conv", "k_fused"),           # HexConv2d 3->3 runs on k_fused MD 1
     "hex_to_rect": ("h2r", "k_h2r_stream"),
     "calib_torch_copy": ("copy", "__amd_rocclr_copyBuffer"),
     "calib_r2h_nearest": ("r2h_nearest", "k_resample_nearest"),
