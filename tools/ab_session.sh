@@ -3,6 +3,5 @@
 set -o pipefail
 TAG=${1:-ab}; mkdir -p gpurun_out/$TAG; O=gpurun_out/$TAG/ab.txt; : > $O
 export TMPDIR=/tmp
-timeout -k 10 200 python3 -u tools/ab_ops.py pyr 15 base ps15 ps45 ps60 >> $O 2>&1 || { cat $O; exit 1; }
-timeout -k 10 200 python3 -u tools/ab_ops.py r2h 15 base >> $O 2>&1 || { cat $O; exit 1; }
+timeout -k 10 200 python3 -u tools/ab_ops.py conv 15 base cvpd4 cvpd2 cvw5 >> $O 2>&1 || { cat $O; exit 1; }
 cat $O
