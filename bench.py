@@ -268,8 +268,9 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": traffic_note,
                 "alg_bytes_per_launch": alg_bytes[dom],
-                "limiter": "VALU issue for the fused kernel: a build whose loads/stores hit one "
-                           "cache-resident row runs as fast (DESIGN.md section 9)"
+                "limiter": "VALU issue for the fused kernel at 3 waves per SIMD: a build whose "
+                           "loads/stores hit one cache-resident row is only 8 % faster "
+                           "(DESIGN.md section 6)"
                 if dom == "pipeline_r2h_conv_h2r" else "hbm"}
 
     compare = None
