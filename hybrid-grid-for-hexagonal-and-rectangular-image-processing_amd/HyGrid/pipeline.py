@@ -70,7 +70,7 @@ def pyramid_fusable(conv):
             and conv.kernel.dtype == torch.float32)
 
 
-def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=False):
+def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=True):
     """Hex Gaussian pyramid (BASELINE config 5): rect -> hex at full size
     (geometry_np.py:358-519), then `levels` x [conv (a HexConv2d, HexFrames.py:96-169)
     -> hexresize to (h//2, w//2) (geometry_np.py:520-681)].  Returns the list of level
@@ -78,11 +78,10 @@ def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=Fals
     x's dtype when 16-bit, else fp32).
 
     With a depthwise radius-2 conv (pyramid_fusable) and no autograd, every level is one
-    pass of hg_hex_pyramid_level after a rect -> hex pass stored in out_dtype (the
-    row-streaming resampler; measured faster than folding rect -> hex into level 0,
-    l0_from_rect=True: 1.71 vs 2.37 ms on config 5, tools/ab_pyramid.py),
-    with the intermediates in fp32 on chip; otherwise the operator chain, which stores
-    every stage in out_dtype.
+    pass of hg_hex_pyramid_level with the intermediates in fp32 on chip; level 0 reads the
+    rect image and makes rect -> hex on the fly (l0_from_rect, the streaming kernel's FR
+    mode: 1.12 vs 1.29 ms for a separate rect -> hex pass on config 5, tools/ab_pyramid.py);
+    otherwise the operator chain, which stores every stage in out_dtype.
     """
     if out_dtype is None:
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32

@@ -34,7 +34,7 @@ namespace hg {
 // pyramid_stream.hip: the register-streaming level for 2x downsamples (HG_EUNSUP otherwise)
 int pyr_stream_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
                    int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
-                   const float* bias, int even_odd_offset, hipStream_t st);
+                   const float* bias, int even_odd_offset, int from_rect, hipStream_t st);
 
 constexpr int PY_THREADS = 256;
 constexpr int PY_TZR = 16;                 // output tile rows
@@ -483,9 +483,9 @@ extern "C" int hg_hex_pyramid_level(const void* src, void* dst, int src_dtype, i
         return HG_EUNSUP;
     if (from_rect && !r2h_near_identity(G.r2h)) return HG_EUNSUP;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (!from_rect) {
+    {
         const int rc = pyr_stream_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1,
-                                      w1, taps, bias, even_odd_offset, st);
+                                      w1, taps, bias, even_odd_offset, from_rect, st);
         if (rc != HG_EUNSUP) return rc;
     }
     switch (src_dtype) {

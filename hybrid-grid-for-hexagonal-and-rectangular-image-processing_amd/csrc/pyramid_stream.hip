@@ -43,13 +43,14 @@ constexpr int PS_OWN = 60;         // output columns per window (lanes 2..61)
 #ifndef PS_RB_
 #define PS_RB_ 30
 #endif
-constexpr int PS_RB = PS_RB_;      // output rows per band (multiple of 5: ring period)
+constexpr int PS_RB = PS_RB_;      // output rows per band (multiple of 5 and 6: ring periods)
 
 struct PyrStreamGeom {
     int64_t B;
     int h, w, h1, w1;
     int nwin, nband;
     Axis xs, ys;                   // hexresize lattice axes (geometry_np.py:570-582)
+    Axis rxs, rys;                 // FR: rect_to_hex lattice axes (h, w) -> (h, w) (:415-422)
     const float* taps;             // [C][7]
     const float* bias;             // [C] or null
 };
@@ -74,7 +75,13 @@ __host__ __device__ constexpr int ps_tap_shift(int t, int par, int op) {
 }
 template <int N> using PIC = std::integral_constant<int, N>;
 
-template <int OP, int C, typename Tin, typename Tout>
+// FR = 1: the level input is the RECT image and X = rect_to_hex(rect) (geometry_np.py:
+// 358-519, bilinear, same size, near-identity lattice) is made on the fly per X row: rows
+// from a 12-row rect ring (one fp32 blend of rect rows in(r), in(r) + 1 with the row weights
+// of a per-wave LDS table), columns from the lane's two columns and one DPP neighbour (the
+// streaming r2h's expressions, k_r2h_stream).  Config 5 then never writes or re-reads the
+// full-size hex image.
+template <int OP, int C, int FR, typename Tin, typename Tout>
 __global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict__ x,
                                                            Tout* __restrict__ y,
                                                            PyrStreamGeom G) {
@@ -108,7 +115,9 @@ __global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict
     const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(y + img * C * opl), (short)0, (int)(C * opl * (int64_t)sizeof(Tout)), 0x00020000);
     const int lc = min(max(ce, 0), G.w - 2);
-    const unsigned xoff = (unsigned)lc * (unsigned)sizeof(Tin);
+    // FR: rect columns outside the raster load as zeros (buffer range check), as the
+    // streaming r2h reads them
+    const unsigned xoff = (FR && !colin) ? 0x80000000u : (unsigned)lc * (unsigned)sizeof(Tin);
     const unsigned yoff = own ? (unsigned)bo * (unsigned)sizeof(Tout) : 0x80000000u;
     const unsigned xplane = (unsigned)(ipl * (int64_t)sizeof(Tin));
     const unsigned yplane = (unsigned)(opl * (int64_t)sizeof(Tout));
@@ -124,9 +133,12 @@ __global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict
 #pragma unroll
     for (int c = 0; c < C; ++c) bv[c] = G.bias ? G.bias[c + vz] : 0.f;
 
-    // ---- input ring: rows 2*a0 - 1 + k in slot k % 10 --------------------------------
-    const int rb0 = 2 * a0 - 1;
-    unsigned raw[10][C];
+    // ---- input ring: rows rb0 + k in slot k % NR ------------------------------------
+    // hex input: rows 2*a0 - 1 ..; FR: rect rows 2*a0 - 2 .. (X rows 2a-1+E .. 2a+2+E need
+    // rect rows 2a-2 .. 2a+4)
+    constexpr int NR = FR ? 12 : 10, PER = NR / 2;      // ring slots, steps per ring period
+    const int rb0 = 2 * a0 - 1 - FR;
+    unsigned raw[NR][C];
     auto issue = [&](auto SLc, int r) {
         constexpr int SL = decltype(SLc)::value;
         const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane(
@@ -144,9 +156,76 @@ __global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict
         o = in ? (float)__builtin_bit_cast(Tin, (unsigned short)(v >> 16)) : 0.f;
     };
 
+    // FR: per-wave table of the r2h rows of X rows 2*a0 - 1 + lane (geometry_np.py:440-449):
+    // {in(r) - r + 1, weight of rect row in+1, weight of row in, validity bits}
+    __shared__ float4 plut_all[PS_THREADS / 64][FR ? 64 : 1];
+    float fjv[2] = {0.f, 0.f}, gjv[2] = {0.f, 0.f};
+    bool leftv[2] = {false, false}, deadv[2] = {true, true};
+    if constexpr (FR) {
+        float4* plut = plut_all[wslot];
+        const int r = 2 * a0 - 1 + lane;
+        float4 t = {0.f, 0.f, 0.f, 0.f};
+        if (r >= 0 && r < G.h) {
+            const double i_ = axis_at(G.rxs, r) + (double)(G.h - 1) * 0.5;
+            const int in = (int)i_;
+            const double fi = i_ - (double)(float)in;
+            t.x = (float)(in - r + 1);
+            t.y = (float)fi;                          // row in + 1 (:515 c0 = fi)
+            t.z = (float)(1.0 - fi);                  // row in
+            t.w = (float)((in >= 0 && in < G.h ? 1 : 0) | (in + 1 >= 0 && in + 1 < G.h ? 2 : 0));
+        }
+        plut[lane] = t;
+        // the lane's two columns (geometry_np.py:441-449): taps jn, jn + 1 with jn - q in
+        // {-1, 0}; a column with no tap inside the raster is dead (both taps read 0)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int q = ce + k;
+            if (q >= 0 && q < G.w) {
+                const double j_ = axis_at(G.rys, q) + (double)(G.w - 1) * 0.5;
+                const int jn = (int)j_;
+                const double jf = j_ - (double)(float)jn;
+                fjv[k] = (float)jf;
+                gjv[k] = (float)(1.0 - jf);
+                leftv[k] = jn < q;
+                deadv[k] = !((jn >= 0 && jn < G.w) || (jn + 1 >= 0 && jn + 1 < G.w));
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);           // lgkmcnt(0): own-wave LDS writes
+        __builtin_amdgcn_wave_barrier();
+    }
+    // FR: X row r (table entry L) from rect rows in(r), in(r)+1 = ring slots S0 + sel, S0 +
+    // sel + 1 (S0 = slot of rect row r - 1), the r2h blend of k_r2h_stream in fp32
+    auto xrow_fr = [&](auto S0c, const float4 L, int r, int c, float& e, float& o) {
+        constexpr int S0 = decltype(S0c)::value;
+        const bool sel = L.x != 0.f;
+        const unsigned ra = sel ? raw[(S0 + 1) % NR][c] : raw[S0][c];
+        const unsigned rbv = sel ? raw[(S0 + 2) % NR][c] : raw[(S0 + 1) % NR][c];
+        const unsigned val = (unsigned)L.w;
+        float ae = (float)__builtin_bit_cast(Tin, (unsigned short)(ra & 0xffffu));
+        float ao = (float)__builtin_bit_cast(Tin, (unsigned short)(ra >> 16));
+        float be = (float)__builtin_bit_cast(Tin, (unsigned short)(rbv & 0xffffu));
+        float bo_ = (float)__builtin_bit_cast(Tin, (unsigned short)(rbv >> 16));
+        if (!(val & 1u)) { ae = 0.f; ao = 0.f; }           // uniform: a dead rect row
+        if (!(val & 2u)) { be = 0.f; bo_ = 0.f; }
+        const float te = L.y * be + L.z * ae, to = L.y * bo_ + L.z * ao;   // :515-516
+        const float tm = ps_prev(to), tp = ps_next(te);   // columns ce - 1, ce + 2
+        const float t1e = deadv[0] ? 0.f : (leftv[0] ? tm : te);
+        const float t2e = deadv[0] ? 0.f : (leftv[0] ? te : to);
+        const float t1o = deadv[1] ? 0.f : (leftv[1] ? te : to);
+        const float t2o = deadv[1] ? 0.f : (leftv[1] ? to : tp);
+        const bool in = colin && r >= 0 && r < G.h;          // X outside the raster: padding
+        e = in ? fjv[0] * t2e + gjv[0] * t1e : 0.f;          // :517
+        o = in ? fjv[1] * t2o + gjv[1] * t1o : 0.f;
+    };
+
     // one output row a (ring offset K = a - a0 mod 5, static); E = i_n(a) - 2a
-    auto step = [&](auto Kc, auto Ec, int a, const double i_, int i_n) {
+    // FR: X rows R0+1, R0+2 of a step, the next step's rows R0-1, R0 when both steps have
+    // E = 0 (each X row is then made once); xc_ok says the cache holds them
+    float xce[2][C], xco[2][C];
+    bool xc_ok = false;
+    auto step = [&](auto Kc, auto Ec, auto CACHEDc, int a, const double i_, int i_n) {
         constexpr int K = decltype(Kc)::value, E = decltype(Ec)::value;
+        constexpr bool CACHED = decltype(CACHEDc)::value;
         // lattice of this (row, lane) (geometry_np.py:601-623)
         const double i_f = i_ - (double)(float)i_n;
         const double j_ = 0.5 * i_ + yv + cw;
@@ -165,14 +244,34 @@ __global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict
         const bool v2 = flag ? (r1in && c1 >= 0 && c1 < G.w) : (c0 + 1 >= 0 && c0 + 1 < G.w);
         const bool v3 = r1in && c1 + 1 >= 0 && c1 + 1 < G.w;
         const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a * yrow));
+        float4 LT[4];                                  // FR: table rows of X rows R0-1 .. R0+2
+        if constexpr (FR) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) LT[k] = plut_all[wslot][2 * (a - a0) + E + k];
+        }
 #pragma unroll
         for (int c = 0; c < C; ++c) {
-            // input rows R0-1 .. R0+2 = 2a-1+E .. 2a+2+E: ring slots (2K+E .. 2K+E+3) % 10
+            // input rows R0-1 .. R0+2 = 2a-1+E .. 2a+2+E: ring slots (2K+E .. 2K+E+3) % 10;
+            // FR: X rows made from rect rows, rect row R0 - 2 + k' in slot (2K+E+k') % 12
             float xe[4], xo[4];
-            xrowf(PIC<(2 * K + E) % 10>{}, R0 - 1, c, xe[0], xo[0]);
-            xrowf(PIC<(2 * K + E + 1) % 10>{}, R0, c, xe[1], xo[1]);
-            xrowf(PIC<(2 * K + E + 2) % 10>{}, R0 + 1, c, xe[2], xo[2]);
-            xrowf(PIC<(2 * K + E + 3) % 10>{}, R0 + 2, c, xe[3], xo[3]);
+            if constexpr (FR) {
+                if constexpr (CACHED) {
+                    xe[0] = xce[0][c]; xo[0] = xco[0][c];
+                    xe[1] = xce[1][c]; xo[1] = xco[1][c];
+                } else {
+                    xrow_fr(PIC<(2 * K + E) % NR>{}, LT[0], R0 - 1, c, xe[0], xo[0]);
+                    xrow_fr(PIC<(2 * K + E + 1) % NR>{}, LT[1], R0, c, xe[1], xo[1]);
+                }
+                xrow_fr(PIC<(2 * K + E + 2) % NR>{}, LT[2], R0 + 1, c, xe[2], xo[2]);
+                xrow_fr(PIC<(2 * K + E + 3) % NR>{}, LT[3], R0 + 2, c, xe[3], xo[3]);
+                xce[0][c] = xe[2]; xco[0][c] = xo[2];
+                xce[1][c] = xe[3]; xco[1][c] = xo[3];
+            } else {
+                xrowf(PIC<(2 * K + E) % NR>{}, R0 - 1, c, xe[0], xo[0]);
+                xrowf(PIC<(2 * K + E + 1) % NR>{}, R0, c, xe[1], xo[1]);
+                xrowf(PIC<(2 * K + E + 2) % NR>{}, R0 + 1, c, xe[2], xo[2]);
+                xrowf(PIC<(2 * K + E + 3) % NR>{}, R0 + 2, c, xe[3], xo[3]);
+            }
             float pe[4], ne[4], no[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -219,19 +318,26 @@ __global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict
         i_ = axis_at(G.xs, a) + ch;
         i_n = __builtin_amdgcn_readfirstlane((int)i_);
     };
-    // step a (= a0 + K + 5m) with its prefetch of input rows 2a+6, 2a+7
+    // step a (= a0 + K + PER m) with its prefetch of input rows 2a+6, 2a+7 (FR: rect rows
+    // 2a+7, 2a+8)
     auto full = [&](auto Kc, int a) {
         constexpr int K = decltype(Kc)::value;
-        issue(PIC<(2 * K + 7) % 10>{}, 2 * a + 6);
-        issue(PIC<(2 * K + 8) % 10>{}, 2 * a + 7);
+        issue(PIC<(2 * K + 7 + 2 * FR) % NR>{}, 2 * a + 6 + FR);
+        issue(PIC<(2 * K + 8 + 2 * FR) % NR>{}, 2 * a + 7 + FR);
         double i_;
         int i_n;
         row_lat(a, i_, i_n);
-        if (i_n == 2 * a) step(Kc, PIC<0>{}, a, i_, i_n);
-        else step(Kc, PIC<1>{}, a, i_, i_n);   // i_n = 2a + 1 (host-checked)
+        if (i_n == 2 * a) {
+            if (FR && xc_ok) step(Kc, PIC<0>{}, std::true_type{}, a, i_, i_n);
+            else step(Kc, PIC<0>{}, std::false_type{}, a, i_, i_n);
+            xc_ok = FR;
+        } else {                                  // i_n = 2a + 1 (host-checked)
+            step(Kc, PIC<1>{}, std::false_type{}, a, i_, i_n);
+            xc_ok = false;
+        }
     };
 
-    // prologue: input rows 2a0-1 .. 2a0+5
+    // prologue: input rows rb0 .. rb0 + 6 (FR: rect rows rb0 .. rb0 + 8)
     issue(PIC<0>{}, rb0);
     issue(PIC<1>{}, rb0 + 1);
     issue(PIC<2>{}, rb0 + 2);
@@ -239,13 +345,18 @@ __global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict
     issue(PIC<4>{}, rb0 + 4);
     issue(PIC<5>{}, rb0 + 5);
     issue(PIC<6>{}, rb0 + 6);
+    if constexpr (FR) {
+        issue(PIC<7>{}, rb0 + 7);
+        issue(PIC<8>{}, rb0 + 8);
+    }
     int a = a0;
-    for (; a + 5 <= a1; a += 5) {
+    for (; a + PER <= a1; a += PER) {
         full(PIC<0>{}, a);
         full(PIC<1>{}, a + 1);
         full(PIC<2>{}, a + 2);
         full(PIC<3>{}, a + 3);
         full(PIC<4>{}, a + 4);
+        if constexpr (PER == 6) full(PIC<5>{}, a + 5);
     }
     if (a < a1) {
         full(PIC<0>{}, a);
@@ -253,7 +364,10 @@ __global__ __launch_bounds__(PS_THREADS) void k_pyr_stream(const Tin* __restrict
             full(PIC<1>{}, a + 1);
             if (a + 2 < a1) {
                 full(PIC<2>{}, a + 2);
-                if (a + 3 < a1) full(PIC<3>{}, a + 3);
+                if (a + 3 < a1) {
+                    full(PIC<3>{}, a + 3);
+                    if (PER == 6 && a + 4 < a1) full(PIC<4>{}, a + 4);
+                }
             }
         }
     }
@@ -290,26 +404,46 @@ static bool ps_lattice_ok(const Geom& g) {
     return qmin + gmin - eps >= -1.0 && qmax + gmax + eps < 2.0;
 }
 
-template <int OP, int C, typename Tin, typename Tout>
+template <int OP, int C, int FR, typename Tin, typename Tout>
 static int ps_launch(const void* src, void* dst, const PyrStreamGeom& G, hipStream_t st) {
     const int64_t blocks = G.B * (int64_t)G.nband * ((G.nwin + 3) / 4);
     if (blocks > INT_MAX) return HG_ESHAPE;
-    hipLaunchKernelGGL((k_pyr_stream<OP, C, Tin, Tout>), dim3((unsigned)blocks), dim3(PS_THREADS),
-                       0, st, (const Tin*)src, (Tout*)dst, G);
+    hipLaunchKernelGGL((k_pyr_stream<OP, C, FR, Tin, Tout>), dim3((unsigned)blocks),
+                       dim3(PS_THREADS), 0, st, (const Tin*)src, (Tout*)dst, G);
     return launch_status();
 }
 
 template <int OP, typename Tin, typename Tout>
-static int ps_channels(const void* src, void* dst, const PyrStreamGeom& G, int C, hipStream_t st) {
-    if (C == 3) return ps_launch<OP, 3, Tin, Tout>(src, dst, G, st);
-    if (C == 1) return ps_launch<OP, 1, Tin, Tout>(src, dst, G, st);
+static int ps_channels(const void* src, void* dst, const PyrStreamGeom& G, int C, int fr,
+                       hipStream_t st) {
+    if (C == 3) return fr ? ps_launch<OP, 3, 1, Tin, Tout>(src, dst, G, st)
+                          : ps_launch<OP, 3, 0, Tin, Tout>(src, dst, G, st);
+    if (C == 1) return fr ? ps_launch<OP, 1, 1, Tin, Tout>(src, dst, G, st)
+                          : ps_launch<OP, 1, 0, Tin, Tout>(src, dst, G, st);
     return HG_EUNSUP;
 }
 
+// FR: the same-size rect -> hex lattice is near-identity (every live tap within one row /
+// column below the sample's own index: in - r, jn - q in {-1, 0}), checked on the lattice
+static bool ps_r2h_near_identity(const Geom& g) {
+    for (int64_t q = 0; q < g.w1; ++q) {
+        const int64_t jn = (int64_t)(axis_at(g.ys, q) + (double)(g.w - 1) * 0.5);
+        const bool live = (jn >= 0 && jn < g.w) || (jn + 1 >= 0 && jn + 1 < g.w);
+        if (live && (jn - q < -1 || jn - q > 0)) return false;
+    }
+    for (int64_t r = 0; r < g.h1; ++r) {
+        const int64_t in = (int64_t)(axis_at(g.xs, r) + (double)(g.h - 1) * 0.5);
+        const bool live = (in >= 0 && in < g.h) || (in + 1 >= 0 && in + 1 < g.h);
+        if (live && (in - r < -1 || in - r > 0)) return false;
+    }
+    return true;
+}
+
 // One pyramid level on the streaming kernel, or HG_EUNSUP (the caller runs k_pyr_level).
+// from_rect: src is the rect image and the level input is its same-size rect_to_hex.
 int pyr_stream_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
                    int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
-                   const float* bias, int even_odd_offset, hipStream_t st) {
+                   const float* bias, int even_odd_offset, int from_rect, hipStream_t st) {
     if (const char* e = getenv("HYGRID_PYRSTREAM")) {   // A/B switch for measurements
         if (e[0] == '0') return HG_EUNSUP;
     }
@@ -330,12 +464,20 @@ int pyr_stream_try(const void* src, void* dst, int src_dtype, int dst_dtype, int
     G.ys = g.ys;
     G.taps = taps;
     G.bias = bias;
+    if (from_rect) {
+        static_assert(2 * PS_RB + 4 <= 64, "the per-wave r2h row table holds 64 X rows");
+        const Geom r = make_r2h(h, w, h, w);
+        if (!ps_r2h_near_identity(r)) return HG_EUNSUP;
+        G.rxs = r.xs;
+        G.rys = r.ys;
+    }
     const int op = (even_odd_offset + 1) & 1;   // tap column class at padding 1
+    const int fr = from_rect ? 1 : 0;
     if (src_dtype == HG_F16)
-        return op ? ps_channels<1, _Float16, _Float16>(src, dst, G, (int)C, st)
-                  : ps_channels<0, _Float16, _Float16>(src, dst, G, (int)C, st);
-    return op ? ps_channels<1, __bf16, __bf16>(src, dst, G, (int)C, st)
-              : ps_channels<0, __bf16, __bf16>(src, dst, G, (int)C, st);
+        return op ? ps_channels<1, _Float16, _Float16>(src, dst, G, (int)C, fr, st)
+                  : ps_channels<0, _Float16, _Float16>(src, dst, G, (int)C, fr, st);
+    return op ? ps_channels<1, __bf16, __bf16>(src, dst, G, (int)C, fr, st)
+              : ps_channels<0, __bf16, __bf16>(src, dst, G, (int)C, fr, st);
 }
 
 }  // namespace hg

@@ -176,24 +176,28 @@ STREAM_CASES = [  # (B, C, h, w): 2x downsamples the row-streaming level kernel 
 @pytest.mark.parametrize("case", STREAM_CASES)
 @pytest.mark.parametrize("off", [0, 1])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-def test_pyramid_level_stream_vs_oracle_and_lds(case, off, dt, monkeypatch):
+@pytest.mark.parametrize("from_rect", [False, True])
+def test_pyramid_level_stream_vs_oracle_and_lds(case, off, dt, from_rect, monkeypatch):
     """k_pyr_stream (pyramid_stream.hip: 16-bit, 2x downsample, bands of 30 output rows,
     windows of 60 output columns) against the fp64 oracle chain within one output rounding
     of the fp32 result, and against the LDS-tiled k_pyr_level (HYGRID_PYRSTREAM=0) within
-    one output rounding: ragged bands / windows, 1 and 3 channels, both tap classes, bias."""
+    one output rounding: ragged bands / windows, 1 and 3 channels, both tap classes, bias;
+    from_rect: the level input made on the fly from the rect image (rect_to_hex,
+    geometry_np.py:358-519, same size) against the oracle's r2h -> conv -> hexresize."""
     B, C, h, w = case
     h1, w1 = h // 2, w // 2
     g = torch.Generator().manual_seed(h * 3 + w + off)
     taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
     bias = (torch.rand((C,), generator=g) - 0.5).to(DEV)
     x = torch.rand((B, C, h, w), generator=g).to(DEV).to(dt)
-    y = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=False)
+    y = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=from_rect)
     monkeypatch.setenv("HYGRID_PYRSTREAM", "0")
-    y_lds = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=False)
+    y_lds = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=from_rect)
     monkeypatch.delenv("HYGRID_PYRSTREAM")
     assert y is not None and y_lds is not None and y.dtype == dt
     xd = x.double().cpu().numpy()
-    c = O.hexconv2d(xd, taps.cpu().double().numpy(), bias.cpu().double().numpy(), off, 2,
+    hx = O.rect_to_hex(xd, (h, w), 1).reshape(xd.shape) if from_rect else xd
+    c = O.hexconv2d(hx, taps.cpu().double().numpy(), bias.cpu().double().numpy(), off, 2,
                     padding=1, groups=C)
     ref = O.hexresize(c, (h1, w1), 1).reshape(B, C, h1, w1)
     ulp = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
