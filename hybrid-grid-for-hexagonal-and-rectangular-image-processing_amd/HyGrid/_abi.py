@@ -8,7 +8,6 @@ There is no CPU fallback: if the library or a HIP device is missing, the call
 raises.  (The CPU restatement under oracle/ is test infrastructure only.)
 """
 import ctypes
-import hashlib
 import os
 
 import torch  # noqa: F401  — load torch's HIP runtime before ours (shared SONAME)
@@ -19,19 +18,7 @@ LIB_PATH = os.environ.get("HYGRID_LIB", os.path.join(_HERE, "_lib", "libhygrid_h
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
 
 
-def kernel_source_digest():
-    """sha256 (16 hex digits) over the kernel sources (csrc/*.hip, *.h, the C-ABI header):
-    the stamp that ties a profile (profiles/*/pmc_traffic.json) to the code it measured,
-    also where no git metadata travels (the GPU box gets a bare snapshot)."""
-    h = hashlib.sha256()
-    inc = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "hygrid.h")
-    files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
-                   if f.endswith((".hip", ".h", "Makefile")))
-    for f in files + ([inc] if os.path.exists(inc) else []):
-        h.update(os.path.basename(f).encode())
-        with open(f, "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+from ._digest import kernel_source_digest  # noqa: E402  (re-exported)
 
 
 # dtype codes (enum hg_dtype)
@@ -54,6 +41,9 @@ _i64, _int, _vp, _dbl = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_
 _RESAMPLE = ([_vp, _vp, _int, _int, _i64, _i64, _i64, _i64, _i64, _int, _vp], _int)
 SIGNATURES = {
     "hg_abi_version": ([], _int),
+    "hg_build_digest": ([], ctypes.c_char_p),
+    "hg_fused_layout": ([_int, ctypes.POINTER(_int), ctypes.POINTER(_int), ctypes.POINTER(_int)],
+                        _int),
     "hg_strerror": ([_int], ctypes.c_char_p),
     "hg_rect_to_hex": _RESAMPLE,
     "hg_hex_to_rect": _RESAMPLE,
@@ -109,8 +99,23 @@ def lib():
         v = L.hg_abi_version()
         if v != ABI_VERSION:
             raise ImportError(f"libhygrid_hip.so ABI {v}, expected {ABI_VERSION}")
+        # refuse a library built from other sources than the tree it is loaded from (a
+        # stale pushed .so must not produce a parity result or a bench line)
+        built, here = L.hg_build_digest().decode(), kernel_source_digest()
+        if built != here:
+            raise ImportError(f"{LIB_PATH} was built from kernel sources {built}, but this "
+                              f"tree's are {here}: rebuild (make -C csrc)")
         _lib = L
     return _lib
+
+
+def fused_layout(md):
+    """(band_rows, window_owned_columns, window_left_halo) of the streaming fused kernel's
+    mode md (0 pipeline, 1 HexConv2d, 2 round trip): where its bands and windows end."""
+    rows, own, halo = _int(), _int(), _int()
+    check(lib().hg_fused_layout(int(md), ctypes.byref(rows), ctypes.byref(own),
+                                ctypes.byref(halo)), "hg_fused_layout")
+    return rows.value, own.value, halo.value
 
 
 def strerror(status):

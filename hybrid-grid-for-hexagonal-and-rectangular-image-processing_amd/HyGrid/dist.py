@@ -81,8 +81,12 @@ def gather_sums(local, out=None, group=None):
     KB per rank, so it prices the RCCL latency, not xGMI bandwidth.
     """
     world = dist.get_world_size(group)
+    shape = (world * local.shape[0],) + tuple(local.shape[1:])
     if out is None:
-        out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
-                          device=local.device)
+        out = torch.empty(shape, dtype=local.dtype, device=local.device)
+    elif (tuple(out.shape) != shape or out.dtype != local.dtype or not out.is_contiguous()
+          or out.device != local.device):
+        raise ValueError(f"gather_sums: out must be a contiguous {shape} {local.dtype} tensor "
+                         f"on {local.device}")
     dist.all_gather_into_tensor(out, local.contiguous(), group=group)
     return out

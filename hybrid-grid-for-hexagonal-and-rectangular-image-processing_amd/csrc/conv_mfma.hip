@@ -13,10 +13,10 @@
 // order, for every input dtype (16-bit inputs are staged as their exact f32 values).
 //
 // Workgroup = 4 waves = 4 consecutive output rows (one per wave: its parity fixes its tap
-// columns) x 64 columns x 64 output channels.  Per chunk of 16 input channels the
-// workgroup stages P (6 rows x 72 columns x 16 channels, padding applied) and the
-// weights (16 x 7 x 64) in LDS; each wave then runs 7 taps x 4 channel quads x
-// (4 x 4 tiles of 16x16) MFMAs into 64 accumulator registers.  Fragment maps
+// columns) x 32 or 64 output channels.  Per chunk of CM_CC = 8 input channels the
+// workgroup stages P (6 rows x 72 columns x 8 channels, padding applied) and the
+// weights (8 x 7 x 64) in LDS; each wave then runs 7 taps x 2 channel quads x
+// (2-4 x 4 tiles of 16x16) MFMAs into up to 64 accumulator registers.  Fragment maps
 // (MI355X_MICROARCH.md / cdna_hip_programming.md §3): A[i=o][k] from lane (k*16 + i),
 // B[k][j=q] from lane (k*16 + j), D[4*(l/16)+v][l%16] in register v of lane l.
 #include <algorithm>
@@ -110,8 +110,8 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma(const Tin* __restri
                 ps[cc * CM_CST + pr * CM_PP + pc] = v;
             }
         }
-        // ---- stage weights W[o0 .. o0+63][c0 .. c0+15][t] as [c][t][o] -------------------
-        // per output channel the chunk's 16 x 7 weights are contiguous: 28 float4 loads
+        // ---- stage weights W[o0 .. o0+63][c0 .. c0+CM_CC-1][t] as [c][t][o] --------------
+        // per output channel the chunk's CM_CC x 7 = 56 weights are contiguous: 14 float4 loads
         for (int e = tid; e < CM_O * (CM_CC * 7 / 4); e += CM_THREADS) {
             const int o = e / (CM_CC * 7 / 4), f = e - o * (CM_CC * 7 / 4);
             const int og = o0 + o;

@@ -102,7 +102,7 @@ int fused_rt_try(const void* x, void* y, int x_dtype, int y_dtype, int64_t plane
     F.rxs = g.xs;
     F.rys = g.ys;
     F.nwin = (int)((w1 + FU_OWN - 1) / FU_OWN);
-    F.nband = (int)((h1 + FU_RB - 1) / FU_RB);
+    F.nband = (int)((h1 + fu_rb(2) - 1) / fu_rb(2));
     const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + 3) / 4);
     if (blocks > INT_MAX) return HG_ESHAPE;
     const dim3 grid((unsigned)blocks), blk(FU_THREADS);
@@ -141,8 +141,12 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
     F.rxs = g.xs;
     F.rys = g.ys;
     F.nwin = (int)((w2 + FU_OWN - 1) / FU_OWN);
-    F.nband = (int)((h2 + FU_RB - 1) / FU_RB);
-#if FU_MIN_INST   // tuning variants: only the headline instantiation (fast rebuilds)
+    F.nband = (int)((h2 + fu_rb(0) - 1) / fu_rb(0));
+#if FU_MIN_INST == 2   // debugging variants: fp32 C = O = 1 only
+    if (x_dtype == HG_F32 && y_dtype == HG_F32 && C == 1 && O == 1 && G == 1)
+        return fused_launch<float, float, 1, 1, 1>(x, kernel, bias, y, F, op, st);
+    return HG_EUNSUP;
+#elif FU_MIN_INST   // tuning variants: only the headline instantiation (fast rebuilds)
     if (x_dtype == HG_BF16 && y_dtype == HG_BF16 && C == 3 && O == 3 && G == 1)
         return fused_launch<__bf16, __bf16, 3, 3, 1>(x, kernel, bias, y, F, op, st);
     return HG_EUNSUP;
@@ -170,3 +174,11 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
 }
 
 }  // namespace hg
+
+extern "C" int hg_fused_layout(int md, int* band_rows, int* win_own, int* win_halo) {
+    if (md < 0 || md > 2 || !band_rows || !win_own || !win_halo) return HG_EINVAL;
+    *band_rows = hg::fu_rb(md);
+    *win_own = hg::FU_OWN;
+    *win_halo = hg::FU_HL;
+    return HG_OK;
+}

@@ -50,7 +50,7 @@ int fused_conv_try(const void* x, const float* kernel, const float* bias, void* 
     F.h = F.h1 = F.h2 = (int)h;
     F.w = F.w1 = F.w2 = (int)w;
     F.nwin = (int)((w + FU_OWN - 1) / FU_OWN);
-    F.nband = (int)((h + FU_RB_CONV - 1) / FU_RB_CONV);
+    F.nband = (int)((h + fu_rb(1) - 1) / fu_rb(1));
     const int op = (off + padding) & 1;
     if (x_dtype == HG_BF16 && y_dtype == HG_BF16)
         return fconv_channels<__bf16, __bf16>(x, kernel, bias, y, F, C, O, G, op, st);

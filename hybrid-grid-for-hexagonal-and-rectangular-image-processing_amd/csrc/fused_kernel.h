@@ -34,7 +34,12 @@ constexpr int FU_OWN = FU_OWN_;       // owned columns per 128-column window
 constexpr int FU_RB = FU_RB_;
 constexpr int FU_RB_CONV = FU_RB_CONV_;
 constexpr int FU_LUT = (FU_RB > FU_RB_CONV ? FU_RB : FU_RB_CONV) + 2;   // row table capacity
+// the one definition of a mode's band length, used by the kernel and the host launchers
 __host__ __device__ constexpr int fu_rb(int md) { return md == 1 ? FU_RB_CONV : FU_RB; }
+static_assert(FU_RB % 6 == 0 && FU_RB_CONV % 6 == 0 && FU_RB > 0 && FU_RB_CONV > 0,
+              "bands are whole 6-step blocks (ring slots x row parities)");
+static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
+              "owned columns are whole lanes with a halo of >= 1 lane on each side");
 
 // Tuning knobs (compile-time; tools/build_fvariant.sh builds variants of this file).
 #ifndef FU_PD
@@ -56,7 +61,8 @@ __host__ __device__ constexpr int fu_rb(int md) { return md == 1 ? FU_RB_CONV : 
 #define FU_STAGE 0                    // 16-bit outputs: stage rows in LDS, store whole 128-B lines
 #endif
 #ifndef FU_SCHED
-#define FU_SCHED 0                    // 1: scheduling barrier between steps (bounds register use)
+#define FU_SCHED 1                    // scheduling barrier between steps (bounds register use: with
+                                      // the packed stencil 126 -> 120 VGPRs, 2.92 -> 2.76 ms A/B)
 #endif
 #ifndef FU_CD
 #define FU_CD 1                       // per-wave column-class specialisation of the r2h taps
@@ -75,6 +81,20 @@ __host__ __device__ constexpr int fu_rb(int md) { return md == 1 ? FU_RB_CONV : 
 #endif
 #ifndef FU_FOLD
 #define FU_FOLD 1                     // MD 0: the h2r 0.75 folded into the conv weights
+#endif
+#ifndef FU_PK
+#define FU_PK 1                       // 7-tap stencil as v_pk_fma_f32 on (even, odd) column pairs
+#endif
+#ifndef FU_WPS
+#define FU_WPS 21                     // PK: the first FU_WPS weight pairs live in SGPRs (v_pk_fma_f32
+                                      // reads an SGPR operand at full rate, unlike v_fmac_f32), the
+                                      // rest in VGPRs; 21 of 32 keeps both register files unspilled
+#endif
+#ifndef FU_BIAS_INIT
+#define FU_BIAS_INIT 0                // debugging: bias as the accumulator's start value
+#endif
+#ifndef FU_ONE_CLASS
+#define FU_ONE_CLASS 0                // ISA inspection: instantiate only the (CD 1, RC 1) loop
 #endif
 
 struct FusedGeom {
@@ -149,7 +169,51 @@ __device__ __forceinline__ void fu_store(float e, float o, __amdgpu_buffer_rsrc_
 }
 
 template <int N> using IC = std::integral_constant<int, N>;
+typedef float fu_f2 __attribute__((ext_vector_type(2)));
+// One packed FMA on the lane's (even, odd) column pair, each half an IEEE fmaf (so the
+// result is bit-identical to two v_fmac_f32): c += w[H] * a, the weight half H of the
+// opaque weight pair broadcast with op_sel.  Written as asm because the compiler, given a
+// splat, materialises it as a separate VGPR pair per weight (126 VGPRs for 63 weights).
+#define FU_PFMA_(SEL, WC)                                                                     \
+    asm("v_pk_fma_f32 %0, %1, %2, %0 " SEL : "+v"(c) : WC(wp), "v"(a))
+template <int H, bool S>
+__device__ __forceinline__ fu_f2 fu_pfma(fu_f2 wp, fu_f2 a, fu_f2 c) {
+    if constexpr (H && S) FU_PFMA_("op_sel:[1,0,0] op_sel_hi:[1,1,1]", "s");
+    else if constexpr (H) FU_PFMA_("op_sel:[1,0,0] op_sel_hi:[1,1,1]", "v");
+    else if constexpr (S) FU_PFMA_("op_sel_hi:[0,1,1]", "s");
+    else FU_PFMA_("op_sel_hi:[0,1,1]", "v");
+    return c;
+}
+#undef FU_PFMA_
+// d = w[H] * a + b[HB]: the same with the bias half HB of a (VGPR) bias pair broadcast
+#define FU_PFMAB_(SEL, WC)                                                                    \
+    asm("v_pk_fma_f32 %0, %1, %2, %3 " SEL : "=v"(d) : WC(wp), "v"(a), "v"(bp))
+template <int H, int HB, bool S>
+__device__ __forceinline__ fu_f2 fu_pfma_b(fu_f2 wp, fu_f2 a, fu_f2 bp) {
+    fu_f2 d;
+    if constexpr (S) {
+        if constexpr (H && HB) FU_PFMAB_("op_sel:[1,0,1] op_sel_hi:[1,1,1]", "s");
+        else if constexpr (H) FU_PFMAB_("op_sel:[1,0,0] op_sel_hi:[1,1,0]", "s");
+        else if constexpr (HB) FU_PFMAB_("op_sel:[0,0,1] op_sel_hi:[0,1,1]", "s");
+        else FU_PFMAB_("op_sel_hi:[0,1,0]", "s");
+    } else {
+        if constexpr (H && HB) FU_PFMAB_("op_sel:[1,0,1] op_sel_hi:[1,1,1]", "v");
+        else if constexpr (H) FU_PFMAB_("op_sel:[1,0,0] op_sel_hi:[1,1,0]", "v");
+        else if constexpr (HB) FU_PFMAB_("op_sel:[0,0,1] op_sel_hi:[0,1,1]", "v");
+        else FU_PFMAB_("op_sel_hi:[0,1,0]", "v");
+    }
+    return d;
+}
+#undef FU_PFMAB_
 __host__ __device__ constexpr int fu_mod(int a, int m) { return ((a % m) + m) % m; }
+// compile-time loop: f(IC<B>{}), f(IC<B+1>{}), ..., f(IC<E-1>{})
+template <int B, int E, typename F>
+__device__ __forceinline__ void fu_sfor(F&& f) {
+    if constexpr (B < E) {
+        f(IC<B>{});
+        fu_sfor<B + 1, E>(f);
+    }
+}
 
 // MD 0: rect -> hex -> HexConv2d -> hex -> rect (the pipeline).  MD 1: HexConv2d alone
 // (radius 2, stride 1, padding 1, pad value 0; HexFrames.py:96-169): the "u rows" are
@@ -167,7 +231,7 @@ void k_fused(const Tin* __restrict__ x,
                                                       Tout* __restrict__ y, FusedGeom F) {
     constexpr int CG = C / G, OG = O / G;
     constexpr int PD = FU_PD;
-    static_assert(PD >= 1 && PD <= 4, "raw ring holds PD + 1 <= 6 rows");
+    static_assert(PD >= 1 && PD <= 5, "raw ring: rows a2+2 .. a2+1+PD in flight in 6 slots");
     using Raw = typename RawOf<Tin>::type;
 
     // The 4 waves of a workgroup take 4 adjacent windows of one (image, band): a group
@@ -289,17 +353,48 @@ void k_fused(const Tin* __restrict__ x,
     int vz = 0;
     asm volatile("" : "+v"(vz));
     // MD 0 with FU_FOLD: the exact same-size h2r is 0.75 z[b] + 0.25 z[b +- 1]
-    // (geometry_np.py:347-354); with the conv weights and bias pre-scaled by 0.75 it is
-    // z'[b] + z'[b +- 1] / 3, one FMA per output column instead of two (fp32-rounding
-    // level difference, well inside the 1e-5 tolerance)
+    // (geometry_np.py:347-354); with z' = 0.75 z it is z'[b] + z'[b +- 1] / 3, one FMA per
+    // output column instead of two (fp32-rounding level difference, well inside 1e-5).  The
+    // scalar stencil pre-scales the conv weights and the bias; the packed one scales the r2h
+    // column weights (u' = 0.75 u) and the bias, so its conv weights stay the raw uniform
+    // loads that live in SGPRs.
     constexpr bool FOLD = FU_FOLD && MD == 0;
-    const float ws_ = FOLD ? 0.75f : 1.f;
-    float wk[O * CG * 7];
+    constexpr bool PKW = FU_PK && MD != 2;
+    const float ws_ = (FOLD && !PKW) ? 0.75f : 1.f;
+    if (FOLD && PKW) {
 #pragma unroll
-    for (int i = 0; i < O * CG * 7; ++i) wk[i] = MD == 2 ? 0.f : kern[i + (FU_WSGPR ? 0 : vz)] * ws_;
+        for (int k = 0; k < 3; ++k) {
+            we[k] *= 0.75f;
+            wo_[k] *= 0.75f;
+        }
+    }
+    constexpr int NW = O * CG * 7;
+    constexpr int NWP = (NW + 1) / 2;
+    constexpr int NWS = PKW ? (FU_WPS < NWP ? FU_WPS : NWP) : 0;   // PK: weight pairs in SGPRs
+    float wk[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const bool uni = FU_WSGPR || i / 2 < NWS;          // uniform load -> SGPR
+        wk[i] = MD == 2 ? 0.f : kern[i + (uni ? 0 : vz)] * ws_;
+    }
+    // PK: the weights as (even, odd)-index pairs, a tap picks its half with op_sel: the
+    // first NWS pairs are the uniform loads themselves (SGPRs), the rest opaque VGPR pairs
+    // (a splat weight alone would take an aligned VGPR pair of its own)
+    fu_f2 wkp[NWP];
+#pragma unroll
+    for (int i = 0; i < NWP; ++i) {
+        wkp[i] = fu_f2{wk[2 * i], 2 * i + 1 < NW ? wk[2 * i + 1] : 0.f};
+        if (PKW && i >= NWS) asm volatile("" : "+v"(wkp[i]));
+    }
     float bv[O];
+    fu_f2 bvp[(O + 1) / 2];             // PK: bias pairs (opaque, op_sel picks the half)
 #pragma unroll
-    for (int o = 0; o < O; ++o) bv[o] = (MD != 2 && bias) ? bias[o + vz] * ws_ : 0.f;
+    for (int o = 0; o < O; ++o) bv[o] = (MD != 2 && bias) ? bias[o + vz] * (FOLD ? 0.75f : 1.f) : 0.f;
+#pragma unroll
+    for (int i = 0; i < (O + 1) / 2; ++i) {
+        bvp[i] = fu_f2{bv[2 * i], 2 * i + 1 < O ? bv[2 * i + 1] : 0.f};
+        if (PKW) asm volatile("" : "+v"(bvp[i]));
+    }
     float c75 = 0.75f, c25 = 0.25f;     // h2r weights as VGPR operands, not literals
     float c13 = 1.f / 3.f;
     asm volatile("" : "+v"(c75), "+v"(c25), "+v"(c13));
@@ -322,6 +417,8 @@ void k_fused(const Tin* __restrict__ x,
         Raw raw[6][C];                      // rect rows in flight, slot (row - s0) % 6
         float XE[3][C], XO[3][C];           // rect rows as f32, slot (row - s0) % 3
         float ZE[3][O], ZO[3][O];           // conv rows being accumulated, slot (row - s0) % 3
+        constexpr bool PK = FU_PK && MD != 2;
+        fu_f2 ZP[3][O];                     // PK: the same rows as (even, odd) pairs
 
         auto issue = [&](auto SLc, int k) {
             constexpr int SL = decltype(SLc)::value;
@@ -386,6 +483,56 @@ void k_fused(const Tin* __restrict__ x,
                 }
                 return;
             }
+            if constexpr (PK) {
+                // Packed stencil: the accumulator of conv row r' is the pair (even, odd
+                // column) and every tap one v_pk_fma_f32 with the weight broadcast by op_sel;
+                // its u operand is the pair at column shift s: (u[ce+s], u[ce+1+s]).
+                // Channel / tap indices are compile-time (fu_sfor) so every weight's register
+                // file (SGPR or VGPR pair) and half are fixed in the instruction.
+                fu_sfor<0, C>([&](auto Cc) {
+                    constexpr int c = decltype(Cc)::value;
+                    const fu_f2 U0 = {ue[c], uo[c]};
+                    // only the shifts this u row's roles use are built (the rest is dead)
+                    const float ne = f_next(ue[c]);
+                    const fu_f2 U1 = {uo[c], ne};
+                    const fu_f2 Um = {f_prev(uo[c]), ue[c]};
+                    const fu_f2 U2 = {ne, OP == 0 ? f_next(uo[c]) : 0.f};
+                    auto at = [&](int s) { return s == -1 ? Um : (s == 0 ? U0 : (s == 1 ? U1 : U2)); };
+                    constexpr int g = c / CG, ci = c % CG;
+                    fu_sfor<0, OG>([&](auto OOc) {
+                        constexpr int o = g * OG + decltype(OOc)::value;
+                        constexpr int j0 = (o * CG + ci) * 7;
+                        // tap t: weight j0 + t is half (j0 + t) & 1 of pair (j0 + t) / 2
+                        auto tap = [&](auto Tc, fu_f2& z, int par) {
+                            constexpr int j = j0 + decltype(Tc)::value;
+                            constexpr bool WS = (j >> 1) < NWS;
+                            const fu_f2 a = at(fu_tap_shift(decltype(Tc)::value, par, OP));
+                            z = fu_pfma<j & 1, WS>(wkp[j >> 1], a, z);
+                        };
+                        if constexpr (ci == 0 && FU_BIAS_INIT) {   // accumulator starts at the bias
+                            ZP[S2][o] = fu_f2{bv[o], bv[o]};
+                            tap(IC<0>{}, ZP[S2][o], PB);
+                        } else if constexpr (ci == 0) {   // the first tap of conv row r+1 adds the bias
+                            constexpr bool WS = (j0 >> 1) < NWS;
+                            ZP[S2][o] = fu_pfma_b<j0 & 1, o & 1, WS>(
+                                wkp[j0 >> 1], at(fu_tap_shift(0, PB, OP)), bvp[o >> 1]);
+                        } else {
+                            tap(IC<0>{}, ZP[S2][o], PB);
+                        }
+                        tap(IC<1>{}, ZP[S2][o], PB);
+                        if constexpr (CEN) {
+                            tap(IC<2>{}, ZP[S1][o], PC);
+                            tap(IC<3>{}, ZP[S1][o], PC);
+                            tap(IC<4>{}, ZP[S1][o], PC);
+                        }
+                        if constexpr (BEL) {
+                            tap(IC<5>{}, ZP[S0][o], PB);
+                            tap(IC<6>{}, ZP[S0][o], PB);
+                        }
+                    });
+                });
+                return;
+            }
     #pragma unroll
             for (int c = 0; c < C; ++c) {
                 // u at column offsets -1 .. 2 of each of the lane's two columns
@@ -439,7 +586,7 @@ void k_fused(const Tin* __restrict__ x,
             const unsigned so = FU_NOMEM ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
     #pragma unroll
             for (int o = 0; o < O; ++o) {
-                const float ze = ZE[S0][o], zo = ZO[S0][o];
+                const float ze = PK ? ZP[S0][o].x : ZE[S0][o], zo = PK ? ZP[S0][o].y : ZO[S0][o];
                 float oe, oo;
                 if constexpr (MD == 1) {            // HexConv2d output row as is
                     oe = ze;
@@ -515,6 +662,7 @@ void k_fused(const Tin* __restrict__ x,
                 if (i == 1) issue(IC<3>{}, s0 + 3);
                 if (i == 2) issue(IC<4>{}, s0 + 4);
                 if (i == 3) issue(IC<5>{}, s0 + 5);
+                if (i == 4) issue(IC<0>{}, s0 + 6);
             }
     #pragma unroll
             for (int c = 0; c < C; ++c) {
@@ -595,7 +743,8 @@ void k_fused(const Tin* __restrict__ x,
         run(IC<0>{}, IC<0>{});
     } else {
         // the common classes get their own loop; mixed windows / bands run the generic one
-        if (FU_CD && cd == 1 && rc == 1) run(IC<1>{}, IC<1>{});
+        if (FU_ONE_CLASS) run(IC<1>{}, IC<1>{});
+        else if (FU_CD && cd == 1 && rc == 1) run(IC<1>{}, IC<1>{});
         else if (FU_CD && cd == 1 && rc == 2) run(IC<1>{}, IC<2>{});
         else if (FU_CD && cd == 2 && rc == 1) run(IC<2>{}, IC<1>{});
         else if (FU_CD && cd == 2 && rc == 2) run(IC<2>{}, IC<2>{});

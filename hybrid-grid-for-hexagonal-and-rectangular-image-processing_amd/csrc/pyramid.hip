@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 #include "lattice.h"
@@ -192,7 +193,18 @@ __global__ __launch_bounds__(PY_THREADS) void k_pyr_level(const Tin* __restrict_
     // a tile whose samples all fall outside the raster still stores its zeros
     const int ry0 = any_valid ? red[0] : 0, cy0 = any_valid ? red[2] : 0;
     const int yr = any_valid ? red[1] - red[0] + 1 : 1, yc = any_valid ? red[3] - red[2] + 1 : 1;
-    if (yr > PY_YR || yc > PY_YC) return;      // host-checked: never for a planned call
+    // Footprint larger than the LDS tile: the host check (pyr_footprint_ok) samples rows and
+    // adds a skew margin, so this is not expected; if it happens, the tile's outputs are
+    // written as NaN rather than left uninitialised, so the failure is visible.
+    auto poison = [&]() {
+        for (int64_t p = p0; p < p1; ++p)
+            for (int k = tid; k < PY_TZR * PY_TZC; k += PY_THREADS) {
+                const int a = a0 + k / PY_TZC, b = b0 + k % PY_TZC;
+                if (a < G.h1 && b < G.w1)
+                    dst[(p * G.h1 + a) * (int64_t)G.w1 + b] = (Tout)__builtin_nanf("");
+            }
+    };
+    if (yr > PY_YR || yc > PY_YC) { poison(); return; }
     int zo[PY_NZ][3];
 #pragma unroll
     for (int i = 0; i < PY_NZ; ++i)
@@ -247,7 +259,7 @@ __global__ __launch_bounds__(PY_THREADS) void k_pyr_level(const Tin* __restrict_
         sa = rin ? floor_even(red[6]) : 0;
         const int sr = rin ? red[5] - red[4] + 1 : 1;
         const int sd = rin ? (red[7] - sa) / EPD + 1 : 1;
-        if (sr > PY_RR || sd * EPD + 1 > PY_RP) return;          // host-checked
+        if (sr > PY_RR || sd * EPD + 1 > PY_RP) { poison(); return; }   // host-checked
         for (int e = tid; e < xr; e += PY_THREADS)
             // rows outside the raster (validity 0) point at tile row 0: read, never used
             rrow[e] = make_int2((rrow_v[e] ? rrow_i[e] - sr0 : 0) | (rrow_v[e] << 28),
@@ -487,6 +499,11 @@ extern "C" int hg_hex_pyramid_level(const void* src, void* dst, int src_dtype, i
         const int rc = pyr_stream_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1,
                                       w1, taps, bias, even_odd_offset, from_rect, st);
         if (rc != HG_EUNSUP) return rc;
+        // test hook: HYGRID_PYRSTREAM=only declines instead of falling back, so a test can
+        // assert that the streaming kernel is what ran
+        if (const char* e = getenv("HYGRID_PYRSTREAM")) {
+            if (e[0] == 'o') return HG_EUNSUP;
+        }
     }
     switch (src_dtype) {
     case HG_F16:

@@ -63,6 +63,16 @@ enum hg_op { HG_OP_RECT_TO_HEX = 0, HG_OP_HEX_TO_RECT = 1, HG_OP_HEXRESIZE = 2 }
 int hg_abi_version(void);
 const char* hg_strerror(int status);
 
+/* The kernel-source digest the library was built from (16 hex digits; the Python loader
+ * refuses a library whose digest differs from its source tree's). */
+const char* hg_build_digest(void);
+
+/* Work decomposition of the streaming fused kernel for mode md (0: hg_pipeline_r2h_conv_h2r,
+ * 1: its HexConv2d mode, 2: hg_pipeline_r2h_h2r): output rows per band, owned columns per
+ * 128-column window and the window's left halo.  Host-only; for tests that place inputs at
+ * band / window edges. */
+int hg_fused_layout(int md, int* band_rows, int* win_own, int* win_halo);
+
 /* rect -> hex lattice resample.
  * Replaces geometry_np.rect_to_hex_resample(rect_image, hex_dsize, interpolation,
  * offset) (HyGrid/geometry_np.py:358-519) for `planes` images at once.

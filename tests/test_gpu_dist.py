@@ -68,3 +68,35 @@ def test_rccl_world1_bench_collectives(nccl_world1):
                             (64, 128), out_dtype=torch.float32)
     ref = rect_hex_conv_rect(mine, conv, out_dtype=torch.float32)
     torch.testing.assert_close(gather_to_root(u), ref, rtol=2 ** -7, atol=2 ** -7)
+
+
+def test_rccl_world1_config3_shard(nccl_world1):
+    """Config 4's per-rank workload through RCCL: one rank's 128 x 3 x 2160 x 3840 bf16 shard
+    (config 3's batch) through the fused pipeline, then the bench's timed-loop collective
+    (per-image sums of every 64th output row, all-gathered into a preallocated buffer) and
+    the checksum gather.  The sums must equal the local ones exactly, and three images of
+    the shard (first, middle, last) are checked against the operator chain."""
+    dev = nccl_world1
+    torch.manual_seed(3)
+    conv = HexConv2d(3, 3, 0, 2, padding=1, bias=True).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(4)
+    x = torch.rand((128, 3, 2160, 3840), generator=gen, device=dev, dtype=torch.bfloat16)
+    mine = local_shard(x)
+    assert mine.shape[0] == 128
+    with torch.no_grad():
+        y = rect_hex_conv_rect(mine, conv, out_dtype=torch.bfloat16)
+    sums = torch.sum(y[:, :, ::64], (2, 3), dtype=torch.float32)
+    buf = torch.empty_like(sums)
+    gs = gather_sums(sums, out=buf)
+    assert gs is buf and torch.equal(gs, sums) and bool(torch.isfinite(gs).all())
+    with pytest.raises(ValueError):
+        gather_sums(sums, out=torch.empty((3, 3), device=dev))
+    cs = gather_checksums(image_checksums(y))
+    assert torch.equal(cs, image_checksums(y))
+    with torch.no_grad():
+        for i in (0, 63, 127):
+            xi = mine[i:i + 1]
+            u = ops.hex_to_rect(conv(ops.rect_to_hex(xi, (2160, 3840), out_dtype=torch.float32)),
+                                (2160, 3840), out_dtype=torch.float32)
+            torch.testing.assert_close(y[i:i + 1].float(), u, rtol=2 ** -7, atol=2 ** -7 * u.abs().max().item())
+    del x, y

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("needs a HIP device", allow_module_level=True)
 
-from HyGrid import ops  # noqa: E402
+from HyGrid import _abi, ops  # noqa: E402
 from HyGrid.HexFrames import HexConv2d  # noqa: E402
 from HyGrid.pipeline import rect_hex_conv_rect  # noqa: E402
 
@@ -140,10 +140,31 @@ def test_non_identity_geometry_falls_back():
     close(y.cpu().numpy(), ref, 1e-5)
 
 
+def edge_points(md, H, W):
+    """Non-finite input points on the streaming kernel's band and window edges for mode md,
+    derived from the library's own decomposition (hg_fused_layout) rather than hard-coded:
+    the last row of every band and the first row of the next one, the last owned column of
+    every window and the first of the next, plus the raster corners."""
+    rows, own, halo = _abi.fused_layout(md)
+    inf, nan = float("inf"), float("nan")
+    vals = [inf, -inf, nan]
+    pts = []
+    edges_r = [r for k in range(1, H // rows + 1) for r in (k * rows - 1, k * rows) if r < H]
+    edges_c = [q for k in range(1, W // own + 1) for q in (k * own - 1, k * own) if q < W]
+    assert len(edges_r) >= 4 and len(edges_c) >= 2, (rows, own, H, W)
+    for i, r in enumerate(edges_r):
+        q = edges_c[i % len(edges_c)]
+        pts.append((i % 3, r, q, vals[i % 3]))
+    pts += [(0, 0, 0, inf), (2, H - 1, W - 1, nan), (1, 3, 50, -inf)]
+    return pts, rows
+
+
 @pytest.mark.parametrize("off", [0, 1])
 def test_fused_nonfinite_inputs_stay_local(off):
-    """Inf / NaN inputs inside the raster, at the 120-column window edges and the 126-row
-    band edges.  The fused kernel evaluates a fixed tap set per column / row class, so a
+    """Inf / NaN inputs inside the raster, on the fused kernel's band edges (last row of a
+    band / first row of the next) and window edges (last owned column of a window / first
+    of the next), placed from hg_fused_layout so they follow the band length the library
+    was built with.  The fused kernel evaluates a fixed tap set per column / row class, so a
     tap whose weight is exactly 0 for one column is still multiplied (0 * Inf = NaN) where
     the reference never reads it; conversely the reference multiplies the same-size h2r's
     zero-weight third vertex (geometry_np.py:347-354) where the fused kernel has no tap.
@@ -153,12 +174,11 @@ def test_fused_nonfinite_inputs_stay_local(off):
     matches the fp64 oracle chain within 1e-5 — the damage stays local."""
     torch.manual_seed(3)
     conv = HexConv2d(3, 3, off, 2, padding=1, bias=True).to(DEV)
-    B, C, H, W = 1, 3, 130, 256
+    rows, own, _ = _abi.fused_layout(0)
+    B, C, H, W = 1, 3, 2 * rows + 14, 2 * own + 16
+    pts, _ = edge_points(0, H, W)
     g = torch.Generator(device=DEV).manual_seed(11)
     x = torch.rand((B, C, H, W), generator=g, device=DEV)
-    inf, nan = float("inf"), float("nan")
-    pts = [(0, 3, 50, inf), (1, H - 4, 77, -inf), (2, 40, 3, inf), (0, 90, W - 4, -inf),
-           (1, 20, 119, nan), (2, 125, 121, inf), (0, 0, 0, inf), (2, H - 1, W - 1, nan)]
     for c, r, q, v in pts:
         x[0, c, r, q] = v
     with torch.no_grad():
@@ -174,3 +194,6 @@ def test_fused_nonfinite_inputs_stay_local(off):
     assert np.isfinite(ref[far]).all() and np.isfinite(got[far]).all()
     scale = np.abs(ref[far]).max()
     np.testing.assert_allclose(got[far], ref[far], rtol=1e-5, atol=1e-5 * scale)
+    # every planted point did reach the output near it (the kernel did not drop an edge row)
+    for _, r, q, _ in pts:
+        assert not np.isfinite(got[:, :, max(r - 3, 0):r + 4, max(q - 3, 0):q + 4]).all()

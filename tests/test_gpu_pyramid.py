@@ -99,6 +99,81 @@ def test_pyramid_8k_full_image_vs_oracle():
     check(outs, [r.reshape(o.shape) for r, o in zip(refs, outs)], 7 * 2 ** -11)
 
 
+def oracle_levels(x, kern, levels=3):
+    """The fused pyramid's storage points: rect -> hex -> conv -> hexresize in fp64 with no
+    rounding inside a level (the kernels keep fp32 intermediates on chip), one fp16
+    rounding per stored level."""
+    rnd = lambda a: a.astype(np.float16).astype(np.float64)  # noqa: E731
+    H, W = x.shape[-2:]
+    cur = O.rect_to_hex(x, (H, W), 1)
+    outs = []
+    h_, w_ = H, W
+    for _ in range(levels):
+        h_, w_ = h_ // 2, w_ // 2
+        cur = rnd(O.hexresize(O.hexconv2d(cur, kern, None, 0, 2, padding=1, groups=3),
+                              (h_, w_), 1))
+        outs.append(cur)
+    return outs
+
+
+def fused_levels_only(x, conv, monkeypatch):
+    """hex_pyramid's fused levels with HYGRID_PYRSTREAM=only: each level must be the
+    row-streaming kernel (level 0 from the rect image), never the LDS fallback."""
+    monkeypatch.setenv("HYGRID_PYRSTREAM", "only")
+    try:
+        H, W = x.shape[-2:]
+        cur, outs, h_, w_ = x, [], H, W
+        with torch.no_grad():
+            for lv in range(3):
+                h_, w_ = h_ // 2, w_ // 2
+                y = ops.hex_pyramid_level(cur, conv.kernel, None, (h_, w_), 0,
+                                          from_rect=(lv == 0), out_dtype=torch.float16)
+                assert y is not None, f"level {lv}: streaming kernel declined {tuple(cur.shape)}"
+                outs.append(y)
+                cur = y
+    finally:
+        monkeypatch.delenv("HYGRID_PYRSTREAM")
+    return outs
+
+
+def test_hex_pyramid_8k_fused_full_size(monkeypatch):
+    """The bench's config-5 path at full size: hex_pyramid on one 4320x7680 fp16 RGB image
+    (level 0 = k_pyr_stream from the rect image, levels 1-2 streaming) against the oracle
+    with fp64 intermediates and one fp16 rounding per stored level; the streaming kernel is
+    asserted to be what ran (HYGRID_PYRSTREAM=only), and hex_pyramid equals it bit for bit.
+    Tolerance: one fp16 rounding per stored level plus fp32 arithmetic, 3 * 2^-11 of max|ref|."""
+    conv = gaussian_conv()
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.rand((1, 3, 4320, 7680), generator=gen, device=DEV, dtype=torch.float16)
+    outs = fused_levels_only(x, conv, monkeypatch)
+    with torch.no_grad():
+        entry = hex_pyramid(x, conv, levels=3)
+    for a, b in zip(entry, outs):
+        assert torch.equal(a, b)
+    refs = oracle_levels(x.double().cpu().numpy(), conv.kernel.detach().cpu().numpy())
+    check(outs, [r.reshape(o.shape) for r, o in zip(refs, outs)], 3 * 2 ** -11)
+
+
+def test_hex_pyramid_8k_batch8_first_last(monkeypatch):
+    """The bench's own launch shape (8 x 3 x 4320 x 7680 fp16, one launch per level): the
+    first and the last image against the oracle (32-bit offset / descriptor range errors at
+    the end of the batch would show here), and every image equals its single-image launch."""
+    conv = gaussian_conv()
+    gen = torch.Generator(device=DEV).manual_seed(8)
+    x = torch.rand((8, 3, 4320, 7680), generator=gen, device=DEV, dtype=torch.float16)
+    outs = fused_levels_only(x, conv, monkeypatch)
+    assert [tuple(o.shape) for o in outs] == [(8, 3, 2160, 3840), (8, 3, 1080, 1920),
+                                              (8, 3, 540, 960)]
+    kern = conv.kernel.detach().cpu().numpy()
+    for i in (0, 7):
+        refs = oracle_levels(x[i:i + 1].double().cpu().numpy(), kern)
+        check([o[i:i + 1] for o in outs], [r.reshape(o[i:i + 1].shape) for r, o in zip(refs, outs)],
+              3 * 2 ** -11)
+        single = fused_levels_only(x[i:i + 1], conv, monkeypatch)
+        for a, b in zip(single, outs):
+            assert torch.equal(a[0], b[i])
+
+
 @pytest.mark.parametrize("H,W", [(540, 960), (136, 250)])
 def test_hex_pyramid_entry_matches_chain(H, W):
     """HyGrid.pipeline.hex_pyramid (the bench's config-5 step) gives the operator chain's
@@ -190,6 +265,7 @@ def test_pyramid_level_stream_vs_oracle_and_lds(case, off, dt, from_rect, monkey
     taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
     bias = (torch.rand((C,), generator=g) - 0.5).to(DEV)
     x = torch.rand((B, C, h, w), generator=g).to(DEV).to(dt)
+    monkeypatch.setenv("HYGRID_PYRSTREAM", "only")   # declines instead of falling back
     y = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=from_rect)
     monkeypatch.setenv("HYGRID_PYRSTREAM", "0")
     y_lds = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=from_rect)

@@ -103,3 +103,31 @@ def test_roundtrip_nonfinite_inputs_stay_local():
     far[..., 27:34, 67:74] = False
     assert bool(torch.isfinite(y[far]).all())
     torch.testing.assert_close(y[far].double(), ref[far], rtol=1e-5, atol=1e-5)
+
+
+def test_roundtrip_nonfinite_at_band_and_window_edges():
+    """MD 2's band / window edges from hg_fused_layout (not hard-coded): non-finite inputs on
+    the last row of a band and the first of the next, on the last owned column of a window
+    and the first of the next; everything farther than 3 samples stays finite and matches
+    the oracle, and every planted point reaches the output next to it."""
+    from HyGrid import _abi
+    rows, own, _ = _abi.fused_layout(2)
+    H, W = 2 * rows + 10, 2 * own + 12
+    g = torch.Generator().manual_seed(7)
+    x = torch.rand((2, 1, H, W), generator=g)
+    vals = [float("nan"), float("inf"), float("-inf")]
+    er = [r for k in (1, 2) for r in (k * rows - 1, k * rows) if r < H]
+    ec = [q for k in (1, 2) for q in (k * own - 1, k * own) if q < W]
+    pts = [(i % 2, r, ec[i % len(ec)]) for i, r in enumerate(er)]
+    for i, (p, r, q) in enumerate(pts):
+        x[p, 0, r, q] = vals[i % 3]
+    y = ops.pipeline_r2h_h2r(x.to(DEV))
+    assert y is not None
+    y = y.cpu()
+    ref = torch.from_numpy(oracle_roundtrip(x))
+    far = torch.ones_like(y, dtype=torch.bool)
+    for p, r, q in pts:
+        far[p, :, max(r - 3, 0):r + 4, max(q - 3, 0):q + 4] = False
+        assert not bool(torch.isfinite(y[p, :, max(r - 3, 0):r + 4, max(q - 3, 0):q + 4]).all())
+    assert bool(torch.isfinite(y[far]).all())
+    torch.testing.assert_close(y[far].double(), ref[far], rtol=1e-5, atol=1e-5)

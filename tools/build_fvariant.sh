@@ -9,7 +9,7 @@ NAME=$1; shift
 OBJ=$PKG/build/obj
 OUT=$PKG/HyGrid/_lib/variants
 mkdir -p "$OUT" "$OBJ/variants"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -DFU_MIN_INST=1 "$@" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -DFU_MIN_INST=${FU_MIN_INST:-1} "$@" \
     -I"$PKG/csrc" -c "${FUSED_SRC:-$PKG/csrc/fused.hip}" -o "$OBJ/variants/fused_$NAME.o"
 # slim library: only what hg_pipeline_r2h_conv_h2r needs (tools/ab_fused.py calls nothing else)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libhygrid_$NAME.so" \
