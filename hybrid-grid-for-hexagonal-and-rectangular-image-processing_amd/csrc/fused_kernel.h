@@ -31,13 +31,21 @@ constexpr int FU_OWN = FU_OWN_;       // owned columns per 128-column window
 #ifndef FU_RB_CONV_
 #define FU_RB_CONV_ 18
 #endif
+#ifndef FU_RB_PYR_
+#define FU_RB_PYR_ 60                 // MD 3 / 4: input rows per band (30 output rows)
+#endif
 constexpr int FU_RB = FU_RB_;
 constexpr int FU_RB_CONV = FU_RB_CONV_;
-constexpr int FU_LUT = (FU_RB > FU_RB_CONV ? FU_RB : FU_RB_CONV) + 2;   // row table capacity
+constexpr int FU_RB_PYR = FU_RB_PYR_;
+constexpr int FU_LUT = (FU_RB > FU_RB_CONV ? (FU_RB > FU_RB_PYR ? FU_RB : FU_RB_PYR)
+                                           : (FU_RB_CONV > FU_RB_PYR ? FU_RB_CONV : FU_RB_PYR)) + 2;
 // the one definition of a mode's band length, used by the kernel and the host launchers
-__host__ __device__ constexpr int fu_rb(int md) { return md == 1 ? FU_RB_CONV : FU_RB; }
-static_assert(FU_RB % 6 == 0 && FU_RB_CONV % 6 == 0 && FU_RB > 0 && FU_RB_CONV > 0,
-              "bands are whole 6-step blocks (ring slots x row parities)");
+__host__ __device__ constexpr int fu_rb(int md) {
+    return md == 1 ? FU_RB_CONV : (md >= 3 ? FU_RB_PYR : FU_RB);
+}
+static_assert(FU_RB % 6 == 0 && FU_RB_CONV % 6 == 0 && FU_RB_PYR % 6 == 0 && FU_RB > 0 &&
+              FU_RB_CONV > 0 && FU_RB_PYR > 0,
+              "bands are whole 6-step blocks (ring slots x row parities), even-aligned");
 static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
               "owned columns are whole lanes with a halo of >= 1 lane on each side");
 
@@ -102,6 +110,7 @@ struct FusedGeom {
     int h, w, h1, w1, h2, w2;
     int nwin, nband;
     Axis rxs, rys;                    // r2h lattice axes (geometry_np.py:415-422)
+    Axis txs, tys;                    // MD 3 / 4: hexresize lattice axes (geometry_np.py:570-582)
 };
 
 __device__ __forceinline__ float f_prev(float v) {   // result[l] = v[l-1], 0 at lane 0
@@ -220,6 +229,11 @@ __device__ __forceinline__ void fu_sfor(F&& f) {
 // the input hex rows themselves and conv rows are stored as they complete.  MD 2: the
 // round trip rect -> hex -> rect without the conv (BASELINE config 2): each u row is its
 // own "conv row" (C == O, no weights) and goes straight through the h2r filter.
+// MD 3 / 4: one hex-pyramid level (BASELINE config 5), the depthwise HexConv2d followed by
+// hexresize to (h / 2, w / 2) (geometry_np.py:520-681) for a 2x downsample: MD 3 from the
+// rect image (u rows made by r2h, as MD 0), MD 4 from a hex image (u rows = input rows, as
+// MD 1).  Every second step completes the two conv rows an output row's triangles read; a
+// window of 128 input columns owns 60 output columns (lane l <-> output column W0/2 + l).
 template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD = 0>
 // MD 1 with 16-bit input and output fits 128 VGPRs (4 waves per SIMD); an fp32 raw ring or
 // fp32 stores need more, and capping those at 128 spills to scratch inside the row loop.
@@ -231,6 +245,8 @@ void k_fused(const Tin* __restrict__ x,
                                                       Tout* __restrict__ y, FusedGeom F) {
     constexpr int CG = C / G, OG = O / G;
     constexpr int PD = FU_PD;
+    constexpr bool PYR = MD >= 3;                 // hex-pyramid level (hexresize output stage)
+    constexpr bool UIN = MD == 1 || MD == 4;      // u rows = input rows (no r2h)
     static_assert(PD >= 1 && PD <= 5, "raw ring: rows a2+2 .. a2+1+PD in flight in 6 slots");
     using Raw = typename RawOf<Tin>::type;
 
@@ -259,13 +275,13 @@ void k_fused(const Tin* __restrict__ x,
     const int ce = W0 + 2 * lane;                 // this lane's even column; odd = ce + 1
     constexpr int RB = fu_rb(MD), NLUT = RB + 2;  // rows per band, u rows band_begin-1 .. +RB
     const int s0 = band * RB;                     // first output row of the band
-    const int s1 = min(s0 + RB, F.h2);
+    const int s1 = min(s0 + RB, PYR ? F.h1 : F.h2);   // PYR: the band walks conv rows
 
     // ---- row table (fp64 lattice math, geometry_np.py:440-486) -------------
     for (int e = lane; e < NLUT; e += 64) {
         const int r = s0 - 1 + e;                 // u row
         float4 t = {0.f, 0.f, 0.f, 0.f};
-        if (MD == 1) {
+        if (UIN) {
             t.y = (r >= 0 && r < F.h) ? 1.f : 0.f;    // u row r = input row r; 0: padding row
         } else if (r >= 0 && r < F.h1) {
             const double i_ = axis_at(F.rxs, r) + (double)(F.h - 1) * 0.5;   // :440
@@ -284,7 +300,7 @@ void k_fused(const Tin* __restrict__ x,
     // (table c == 0), RC 2 if rows r, r+1 (a == 0): two terms per vertical blend instead
     // of three.  A same-size lattice switches class once, in the middle band.
     int rc = 0;
-    if (MD != 1 && FU_RC) {
+    if (!UIN && FU_RC) {
         bool has_a = false, has_c = false;
         for (int e = lane; e < NLUT; e += 64) {
             const float4 t = lut[e];
@@ -300,7 +316,7 @@ void k_fused(const Tin* __restrict__ x,
     // r2h (geometry_np.py:441-449, 514-517): u[q] = sum_k wr_k[q] v[q+k], k = -1..1
     float we[3] = {0.f, 0.f, 0.f}, wo_[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 2 && MD != 1; ++s) {
+    for (int s = 0; s < 2 && !UIN; ++s) {
         const int q = ce + s;
         float* wr = s ? wo_ : we;
         if (q >= 0 && q < F.w1) {
@@ -321,8 +337,16 @@ void k_fused(const Tin* __restrict__ x,
     const float wn_o = (ce + 2 < F.w2) ? 0.25f : 0.f;   // even row, z[b+1], b = ce+1
     const float wp_e = (ce - 1 >= 0) ? 0.25f : 0.f;     // odd row,  z[b-1], b = ce
     const bool colin = ce >= 0 && ce < F.w;           // MD 1: input columns inside (w even)
-    const bool own = lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2 && ce >= 0 && ce < F.w2 &&
-                     win < F.nwin;
+    const int bo = W0 / 2 + lane;                     // PYR: this lane's output column
+    const bool own = PYR ? (lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2 && bo < F.w2 &&
+                            win < F.nwin)
+                         : (lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2 && ce >= 0 &&
+                            ce < F.w2 && win < F.nwin);
+    // PYR: per-lane hexresize lattice constants (geometry_np.py:570-602) on the conv image
+    // (h1, w1): j_ = 0.5 i_ + y_(b) + (w1 - 0.5) / 2 per output row
+    const double t_yv = PYR ? axis_at(F.tys, min(max(bo, 0), F.w2 - 1)) : 0.0;
+    const double t_cw = ((double)F.w1 - 0.5) * 0.5;
+    const double t_ch = (double)(F.h1 - 1) * 0.5;
     // staging slot of this lane's two output columns (non-owned lanes write a pad dword)
     const int sidx = (lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2)
                          ? wslot * (FU_OWN / 2) + lane - FU_HL / 2 : GDW + (lane & 3);
@@ -336,7 +360,7 @@ void k_fused(const Tin* __restrict__ x,
     const int lc = min(max(ce, 0), F.w - 2);            // clamped even load column
     // one VGPR offset per lane; the plane of a channel is an SGPR offset
     const unsigned xoff = (unsigned)lc * (unsigned)sizeof(Tin);
-    const unsigned yoff = own ? (unsigned)ce * (unsigned)sizeof(Tout) : 0x80000000u;
+    const unsigned yoff = own ? (unsigned)(PYR ? bo : ce) * (unsigned)sizeof(Tout) : 0x80000000u;
     const unsigned xplane = (unsigned)(cstride * (int64_t)sizeof(Tin));
     const unsigned yplane = (unsigned)(ostride * (int64_t)sizeof(Tout));
     const unsigned xrow = (unsigned)F.w * (unsigned)sizeof(Tin);
@@ -418,7 +442,9 @@ void k_fused(const Tin* __restrict__ x,
         float XE[3][C], XO[3][C];           // rect rows as f32, slot (row - s0) % 3
         float ZE[3][O], ZO[3][O];           // conv rows being accumulated, slot (row - s0) % 3
         constexpr bool PK = FU_PK && MD != 2;
+        static_assert(PK || !PYR, "the pyramid modes use the packed stencil");
         fu_f2 ZP[3][O];                     // PK: the same rows as (even, odd) pairs
+        fu_f2 ZK[PYR ? O : 1];              // PYR: conv row 2a, kept for output row a
 
         auto issue = [&](auto SLc, int k) {
             constexpr int SL = decltype(SLc)::value;
@@ -442,7 +468,7 @@ void k_fused(const Tin* __restrict__ x,
             constexpr int PB = fu_mod(PH, 2);       // parity of conv row r-1 (and r+1)
             constexpr int PC = 1 - PB;              // parity of conv row r
             float ue[C], uo[C];
-            if constexpr (MD == 1) {                // u = input row, 0 outside (padding 1, value 0)
+            if constexpr (UIN) {                    // u = input row, 0 outside (padding 1, value 0)
                 const bool in_ = colin && L.y != 0.f;
     #pragma unroll
                 for (int c = 0; c < C; ++c) {
@@ -578,11 +604,71 @@ void k_fused(const Tin* __restrict__ x,
             }
         };
 
+        // PYR: output row a of hexresize (geometry_np.py:601-678) from conv rows R0 = i_n(a)
+        // and R1 = R0 + 1: R0 = 2a (ZK) and R1 = 2a + 1 (Z1), or, for the one row with
+        // i_n(a) = 2a + 1 (the last, host-checked: R1 is then outside the raster), R0 = Z1.
+        // The triangle (:612-648): p1 = (R0, c0), p2 = (R1, c1) if i_f > j_f else
+        // (R0, c0 + 1), p3 = (R1, c1 + 1), c0 = j_n - (i_n + 1) // 2, c1 = j_n - (i_n + 2) // 2;
+        // c0 - 2b in {-1, 0, 1} and c1 - 2b in {-2 .. 1} (host-checked), so each vertex is
+        // the lane's own conv value or a neighbour lane's, picked with selects; vertices
+        // outside the raster read 0 (:636-648).  Weights: the barycentric coordinates in the
+        // lattice's (i, j) index frame (an affine image of the reference's Cartesian frame,
+        // :651-678): (1 - i_f, i_f - j_f, j_f) if i_f > j_f, else (1 - j_f, j_f - i_f, i_f).
+        auto pyr_out = [&](const fu_f2 (&Z1)[O], int a) {
+            const double i_ = axis_at(F.txs, a) + t_ch;                  // uniform
+            const int i_n = __builtin_amdgcn_readfirstlane((int)i_);
+            const bool e1 = i_n != 2 * a;                                // uniform
+            const double i_f = i_ - (double)(float)i_n;
+            const double j_ = 0.5 * i_ + t_yv + t_cw;
+            const int j_n = (int)j_;
+            const double j_f = j_ - (double)(float)j_n;
+            const bool flag = i_f > j_f;
+            const float wa = (float)(flag ? 1.0 - i_f : 1.0 - j_f);
+            const float wb = (float)(flag ? i_f - j_f : j_f - i_f);
+            const float wg = (float)(flag ? j_f : i_f);
+            const int c0 = j_n - (i_n + 1) / 2, c1 = j_n - (i_n + 2) / 2;
+            const int d0 = c0 - 2 * bo, d1 = c1 - 2 * bo;
+            const bool r1in = i_n + 1 < F.h1;
+            const bool v1 = c0 >= 0 && c0 < F.w1;
+            const bool v2 = flag ? (r1in && c1 >= 0 && c1 < F.w1) : (c0 + 1 >= 0 && c0 + 1 < F.w1);
+            const bool v3 = r1in && c1 + 1 >= 0 && c1 + 1 < F.w1;
+            const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a * yrow));
+    #pragma unroll
+            for (int o = 0; o < O; ++o) {
+                const fu_f2 z0 = e1 ? Z1[o] : ZK[o], z1 = Z1[o];
+                const float y0pm = f_prev(z0.y), y0ne = f_next(z0.x);
+                const float y1pe = f_prev(z1.x), y1po = f_prev(z1.y), y1ne = f_next(z1.x);
+                const float p1 = d0 < 0 ? y0pm : (d0 == 0 ? z0.x : z0.y);
+                const float p2a = d0 < 0 ? z0.x : (d0 == 0 ? z0.y : y0ne);
+                const float p2b = d1 < -1 ? y1pe : (d1 == -1 ? y1po : (d1 == 0 ? z1.x : z1.y));
+                const float p3 = d1 < -1 ? y1po : (d1 == -1 ? z1.x : (d1 == 0 ? z1.y : y1ne));
+                const float q1 = v1 ? p1 : 0.f;
+                const float q2 = v2 ? (flag ? p2b : p2a) : 0.f;
+                const float q3 = v3 ? p3 : 0.f;
+                const float z = fmaf(wg, q3, fmaf(wb, q2, wa * q1));
+                if constexpr (sizeof(Tout) == 2)
+                    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (Tout)z),
+                                                          yrs, yoff, so + o * yplane, 0);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, z), yrs, yoff,
+                                                          so + o * yplane, 0);
+            }
+        };
+
         // conv row a2 (slot PH % 3, parity PH % 2) -> output row a2 (exact same-size h2r)
         auto out_row = [&](auto PHc, auto SBc, int a2) {
             constexpr int PH = decltype(PHc)::value;
             constexpr int SB = STAGE ? decltype(SBc)::value : 0;
             constexpr int S0 = PH % 3;
+            if constexpr (PYR) {
+                if constexpr ((PH & 1) == 0) {      // conv row 2a: kept for the next step
+    #pragma unroll
+                    for (int o = 0; o < O; ++o) ZK[o] = ZP[S0][o];
+                } else {                            // conv row 2a + 1: output row a
+                    pyr_out(ZP[S0], a2 >> 1);
+                }
+                return;
+            }
             const unsigned so = FU_NOMEM ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
     #pragma unroll
             for (int o = 0; o < O; ++o) {
@@ -738,7 +824,7 @@ void k_fused(const Tin* __restrict__ x,
             tail(IC<0>{}, base);
         }
     };
-    if constexpr (MD == 1) {
+    if constexpr (UIN) {
         (void)cd; (void)rc;
         run(IC<0>{}, IC<0>{});
     } else {

@@ -36,6 +36,10 @@ namespace hg {
 int pyr_stream_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
                    int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
                    const float* bias, int even_odd_offset, int from_rect, hipStream_t st);
+// pyramid_fused.hip: the same level on the streaming fused kernel (tried first)
+int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
+                  int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
+                  const float* bias, int even_odd_offset, int from_rect, hipStream_t st);
 
 constexpr int PY_THREADS = 256;
 constexpr int PY_TZR = 16;                 // output tile rows
@@ -496,11 +500,14 @@ extern "C" int hg_hex_pyramid_level(const void* src, void* dst, int src_dtype, i
     if (from_rect && !r2h_near_identity(G.r2h)) return HG_EUNSUP;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     {
-        const int rc = pyr_stream_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1,
-                                      w1, taps, bias, even_odd_offset, from_rect, st);
+        int rc = pyr_fused_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1, w1,
+                               taps, bias, even_odd_offset, from_rect, st);
         if (rc != HG_EUNSUP) return rc;
-        // test hook: HYGRID_PYRSTREAM=only declines instead of falling back, so a test can
-        // assert that the streaming kernel is what ran
+        rc = pyr_stream_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1,
+                            w1, taps, bias, even_odd_offset, from_rect, st);
+        if (rc != HG_EUNSUP) return rc;
+        // test hook: HYGRID_PYRSTREAM=only declines instead of falling back to the LDS kernel,
+        // so a test can assert that a streaming kernel (fused or k_pyr_stream) is what ran
         if (const char* e = getenv("HYGRID_PYRSTREAM")) {
             if (e[0] == 'o') return HG_EUNSUP;
         }

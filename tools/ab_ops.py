@@ -2,8 +2,9 @@
 (one process, same device buffers, HIP events on the launch stream; median / min per launch).
 
 usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
-  OP: r2h | h2r | conv | r2h32 | h2r32 | pyr   (bf16 4K b128 for r2h/h2r/conv; fp32 1080p b32
-      for r2h32/h2r32; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K)
+  OP: r2h | h2r | conv | r2h32 | h2r32 | pyr | pyrfr | pyr1   (bf16 4K b128 for r2h/h2r/conv;
+      fp32 1080p b32 for r2h32/h2r32; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K from a
+      hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K)
   name 'base' = the in-tree library; others = HyGrid/_lib/variants/libhygrid_<name>.so;
   'name%VAR=VAL' runs that library with the environment variable VAR=VAL set around its calls
   (the library's A/B switches, e.g. base%HYGRID_PYRSTREAM=0)
@@ -41,10 +42,12 @@ def main():
         B, C, H, W, t = 128, 3, 2160, 3840, torch.bfloat16
     elif op in ("r2h32", "h2r32"):
         B, C, H, W, t = 32, 3, 1080, 1920, torch.float32
+    elif op == "pyr1":
+        B, C, H, W, t = 8, 3, 2160, 3840, torch.float16
     else:
         B, C, H, W, t = 8, 3, 4320, 7680, torch.float16
     x = torch.rand((B, C, H, W), generator=g, device=dev, dtype=t)
-    if op == "pyr":
+    if op.startswith("pyr"):
         y = torch.empty((B, C, H // 2, W // 2), device=dev, dtype=t)
         taps = (torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32, device=dev) / 12).repeat(C)
     else:
@@ -70,7 +73,7 @@ def main():
         f = lib.hg_hex_pyramid_level
         f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 6 + [_vp, _vp, _int, _int, _vp]
         return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B, C, H, W, H // 2, W // 2,
-                 taps.data_ptr(), None, 0, 0, s)
+                 taps.data_ptr(), None, 0, 1 if op == "pyrfr" else 0, s)
 
     times = {n: [] for n in names}
     sums = {}
