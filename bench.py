@@ -73,6 +73,9 @@ def parse():
                     help="skip the secondary config-2 line (1080p fp32 rect->hex->rect)")
     ap.add_argument("--no-wide-conv", action="store_true",
                     help="skip the secondary wide-channel HexConv2d line (64->64, 1080p)")
+    ap.add_argument("--no-lattices", action="store_true",
+                    help="skip the reference entry points' own (non-identity) lattices")
+    ap.add_argument("--lattice-batch", type=int, default=32, help="4K images per lattice line")
     ap.add_argument("--pyramid-batch", type=int, default=8, help="8K images per GPU (config 5)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-kernel HBM bytes from rocprofv3 PMC passes (optional)")
@@ -163,6 +166,59 @@ def cpu_baseline(args, kernel, bias):
                                    "what": "the reference's own geometry_np + HexFrames "
                                            "(NumPy, one core), one 4K RGB image, survey "
                                            "container (BASELINE.md section 2)"}}
+
+
+def touched_rows_bytes(ops, op, h, w, h1, w1, dev, nearest, elem):
+    """Bytes of the source rows a resample's lattice references (every referenced row is
+    read once, whole: its cache lines are streamed), from the kernel's own integer maps."""
+    m = ops.lattice_maps(op, h, w, h1, w1, device=dev)
+    i_n, valid = m["i_n"].long(), m["valid"].long()
+    if nearest:
+        rows = i_n + (m["argmin"].long() >> 1)
+        rows = rows[((valid >> m["argmin"].long()) & 1) == 1]
+    else:   # taps (i_n, .) valid bits 0/1, (i_n + 1, .) bits 2/3
+        rows = torch.cat([i_n[(valid & 3) != 0], (i_n + 1)[(valid & 12) != 0]])
+    n = int(torch.unique(rows).numel())
+    return n * w * elem
+
+
+def bench_lattices(ops, measure, gen, dev, world, Bl, C, H, W):
+    """The reference's own entry-point lattices, which are not the same-size one the fused
+    kernel covers: IMAGE.ConvertToHexagon (Image.py:111-116: rect -> hex at (h//2, w//2),
+    'nearest', the image's own dtype, u8 here) and the geometry_np demo's bilinear
+    downsample (geometry_np.py:772-776: an ADE image to (256, 341), ratio ~2; bf16 here), on
+    4K RGB batches.  Algorithmic bytes = the source rows the lattice references (whole rows)
+    + the output; each line carries its own fraction of the 8 TB/s peak."""
+    hs, ws = H // 2, W // 2
+    xu8 = torch.randint(0, 256, (Bl, C, H, W), generator=gen, device=dev, dtype=torch.uint8)
+    xbf = torch.rand((Bl, C, H, W), generator=gen, device=dev, dtype=torch.bfloat16)
+    out = {}
+    cases = (("convert_to_hexagon", xu8, 0, 1, "Image.py:111-116: rect->hex (h//2, w//2) nearest, u8"),
+             ("r2h_bilinear_2x", xbf, 1, 2, "geometry_np.py:772-776 ratio: rect->hex (h//2, w//2) bilinear, bf16"))
+    for name, xin, interp, elem, what in cases:
+        def run(record, ev, xin=xin, interp=interp):
+            if record:
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                e[0].record()
+            y = ops.rect_to_hex(xin, (hs, ws), interp=interp)
+            if record:
+                e[1].record()
+                ev.append(e)
+            return y
+        steps = 10
+        _, el, sms = measure(run, steps, 2, collective=False)
+        rb = touched_rows_bytes(ops, "rect_to_hex", H, W, hs, ws, dev, interp == 0, elem)
+        alg = Bl * C * (rb + hs * ws * elem)
+        out[name] = {"what": what, "batch_per_gpu": Bl, "in_shape": [Bl, C, H, W],
+                     "out_shape": [Bl, C, hs, ws], "ms": round(sms[0], 4),
+                     "value": round(world * Bl * hs * ws * steps / el / 1e6, 1),
+                     "unit": "Mpix/s (output samples)",
+                     "alg_GB": round(alg / 1e9, 4),
+                     "src_rows_referenced_frac": round(rb / (H * W * elem), 4),
+                     "GB_per_s": round(alg / (sms[0] * 1e-3) / 1e9, 1),
+                     "frac_of_peak": round(alg / (sms[0] * 1e-3) / PEAK_BPS, 4)}
+    del xu8, xbf
+    return out
 
 
 def main():
@@ -483,9 +539,11 @@ def main():
     wide = None
     if not args.unfused and not args.no_wide_conv:
         # HexConvModule-sized HexConv2d (HexModules.py:97-288): 64 -> 64 channels on a
-        # 1080p bf16 batch of 4, the implicit GEMM on the f32 matrix cores (conv_mfma.hip).
-        # Compute-bound: reported in TFLOP/s (2 * O * 7 * C per output sample) against the
-        # f32 MFMA peak (157.3 TF, MI355X_MICROARCH.md).  Beside `value`, never as it.
+        # 1080p bf16 batch of 4, the implicit GEMM on the bf16 matrix cores with every fp32
+        # weight split into three bf16 parts (conv_mfma.hip, k_hexconv_mfma_bf16: exact
+        # products, fp32 accumulation).  Compute-bound: algorithmic TFLOP/s (2 * O * 7 * C per
+        # output sample) and the MFMA work actually issued (x 3 weight parts x 8/7 for the
+        # zero eighth tap slot) against the dense bf16 MFMA peak.  Beside `value`, never as it.
         Bw, Cw, Ow, Hw, Ww = 4, 64, 64, 1080, 1920
         xw = (torch.rand((Bw, Cw, Hw, Ww), generator=gen, device=dev) - 0.5).to(bf16)
         torch.manual_seed(5)
@@ -506,13 +564,21 @@ def main():
         _, el_w, sms_w = measure(run_wide, steps_w, 1, collective=False)
         flop = 2.0 * Ow * 7 * Cw * Bw * Hw * Ww
         tf = flop / (sms_w[0] * 1e-3) / 1e12
+        issued = tf * 3 * 8 / 7
         wide = {"workload": f"HexConv2d({Cw},{Ow},0,2,padding=1) bf16, {Bw}x{Cw}x{Hw}x{Ww}",
                 "ms": round(sms_w[0], 4), "TFLOP_s": round(tf, 2),
-                "roofline": {"bound": "mfma", "peak": 157.3, "unit": "TFLOP/s",
-                             "frac": round(tf / 157.3, 4),
-                             "note": "f32 MFMA (exact fp32 products; 16-bit inputs staged "
-                                     "as f32)"}}
+                "vs_f32_mfma_peak": round(tf / 157.3, 4),
+                "roofline": {"bound": "mfma", "achieved": round(issued, 1), "peak": 2500.0,
+                             "unit": "TFLOP/s", "frac": round(issued / 2500.0, 4),
+                             "note": "bf16 MFMA work issued (3 bf16 weight parts x 8/7 tap "
+                                     "slots x the algorithmic flops) vs the dense bf16 peak; "
+                                     "the algorithm's own ceiling is 2500 / 3 / (8/7) = 729 "
+                                     "TFLOP/s of fp32-exact conv"}}
         del xw
+
+    lattices = None
+    if not args.unfused and not args.no_lattices:
+        lattices = bench_lattices(ops, measure, gen, dev, world, args.lattice_batch, C, H, W)
 
     # checksums over RCCL (not timed), and the full-output gather on its own
     from HyGrid.dist import gather_checksums, gather_to_root, image_checksums
@@ -562,6 +628,7 @@ def main():
                        "fused": not args.unfused},
             "kernels": kernels, "roofline": roofline, "cpu_baseline": cpu,
             "unfused": compare, "roundtrip": roundtrip, "pyramid": pyramid, "wide_conv": wide,
+            "lattices": lattices,
             "gather": gather, "checksum": checksum,
             "device": torch.cuda.get_device_name(dev),
         }

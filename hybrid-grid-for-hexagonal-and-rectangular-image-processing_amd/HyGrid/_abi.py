@@ -25,6 +25,7 @@ from ._digest import kernel_source_digest  # noqa: E402  (re-exported)
 HG_U8, HG_I8, HG_U16, HG_I16, HG_I32, HG_I64, HG_F16, HG_BF16, HG_F32, HG_F64 = range(10)
 HG_NEAREST, HG_LINEAR = 0, 1
 HG_OP_RECT_TO_HEX, HG_OP_HEX_TO_RECT, HG_OP_HEXRESIZE = 0, 1, 2
+HG_KERNEL_GENERAL, HG_KERNEL_NEAREST, HG_KERNEL_STREAM, HG_KERNEL_DOWN = range(4)
 PAD_MODES = {"constant": 0, "zeros": 0, "reflect": 1, "replicate": 2, "circular": 3}
 HG_ACT_NONE, HG_ACT_RELU, HG_ACT_LEAKY_RELU, HG_ACT_RELU6, HG_ACT_SIGMOID, HG_ACT_TANH = range(6)
 
@@ -50,6 +51,7 @@ SIGNATURES = {
     "hg_hexresize": _RESAMPLE,
     "hg_resample_backward": ([_int, _vp, _vp, _int] + [_i64] * 5 + [_int, _vp], _int),
     "hg_lattice_maps": ([_int, _i64, _i64, _i64, _i64, _vp, _vp, _vp], _int),
+    "hg_resample_kernel": ([_int, _int, _int] + [_i64] * 5 + [_int], _int),
     "hg_hexconv2d_out_shape": ([_i64, _i64, _int, _int, _int, _int,
                                 ctypes.POINTER(_i64), ctypes.POINTER(_i64)], _int),
     "hg_hexconv2d": ([_vp, _vp, _vp, _vp, _int, _int, _int, _i64, _i64, _i64, _i64, _i64,
@@ -116,6 +118,15 @@ def fused_layout(md):
     check(lib().hg_fused_layout(int(md), ctypes.byref(rows), ctypes.byref(own),
                                 ctypes.byref(halo)), "hg_fused_layout")
     return rows.value, own.value, halo.value
+
+
+def resample_kernel(op, src_dtype, dst_dtype, planes, h, w, h1, w1, interp=HG_LINEAR):
+    """Which kernel a resample call would run (HG_KERNEL_*; nothing is launched)."""
+    st = lib().hg_resample_kernel(int(op), int(src_dtype), int(dst_dtype), int(planes), int(h),
+                                  int(w), int(h1), int(w1), int(interp))
+    if st < 0:
+        check(st, "hg_resample_kernel")
+    return st
 
 
 def strerror(status):

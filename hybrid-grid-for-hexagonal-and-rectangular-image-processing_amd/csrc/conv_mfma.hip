@@ -182,6 +182,147 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma(const Tin* __restri
         }
 }
 
+typedef __bf16 cm_b8 __attribute__((ext_vector_type(8)));
+typedef unsigned cm_u4 __attribute__((ext_vector_type(4)));
+constexpr int CB_PP = 72;                   // staged columns (as CM_PP)
+constexpr int CB_PSZ = CM_PR * CB_PP + 1;   // P fragments per chunk (+1: the zero fragment)
+
+template <typename Tout, int NOT>
+__global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16(const __bf16* __restrict__ x,
+                                                                  const float* __restrict__ kern,
+                                                                  const float* __restrict__ bias,
+                                                                  Tout* __restrict__ y, MfmaGeom G) {
+    constexpr int CM_O = 16 * NOT;                       // output channels of this workgroup
+    // P chunk: [row][col] fragments of the 8 channels (16 B each, channel innermost);
+    // weights: [part][kb][o][g] fragments of the 8 channels of tap 4 kb + g
+    __shared__ cm_u4 psb[CB_PSZ];
+    __shared__ cm_u4 wsb[3 * 2 * CM_O * 4];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    unsigned bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int tq = (int)(bid % G.ntq); bid /= G.ntq;
+    const int tr = (int)(bid % G.ntr); bid /= G.ntr;
+    const int to = (int)(bid % G.nto);
+    const int64_t b = bid / G.nto;
+    const int q0 = tq * CM_Q, r0 = tr * CM_ROWS, o0 = to * CM_O;
+    const int r = r0 + wv;
+    const int par = r & 1;
+    const int Wp = G.w + 2 * G.p, Hp = G.h + 2 * G.p;
+    const int li = lane & 15, lg = lane >> 4;            // fragment row / column, k group
+    const unsigned short padv = __builtin_bit_cast(unsigned short, (__bf16)G.pad_value);
+
+    cm_f4 acc[NOT][4];
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int o = o0 + ot * 16 + lg * 4 + v;
+            const float bv = (bias && o < G.O) ? bias[o] : 0.f;
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt) acc[ot][qt][v] = bv;
+        }
+    }
+    if (tid == 0) psb[CB_PSZ - 1] = cm_u4{0u, 0u, 0u, 0u};
+    // this lane's P fragment (per k block and column tile): tap t = 4 kb + lg, row wv + dy_t,
+    // column qt * 16 + li + dk_t; the 8th tap slot reads the zero fragment
+    int pidx[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        const int t = 4 * kb + lg;
+        pidx[kb] = t < 7 ? (wv + G.dy[t]) * CB_PP + li + (par ? G.dk[1][t] : G.dk[0][t]) : -1;
+    }
+
+    const unsigned short* xb = reinterpret_cast<const unsigned short*>(x) + b * (int64_t)G.C * G.h * G.w;
+    for (int c0 = 0; c0 < G.C; c0 += CM_CC) {
+        // ---- stage P rows r0 .. r0+5, columns q0 + mink + (0..71), 8 channels ------------
+        if (tid < 3 * CB_PP) {
+            const int pc = tid % CB_PP, ph = tid / CB_PP;
+            const int px = q0 + G.mink + pc;
+            const bool zc = px >= Wp;                        // type1 structural zero column
+            const int64_t xi = zc ? -1 : pad_map(px - G.p, G.w, G.pad_mode);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int pr = ph + 3 * k, py = r0 + pr;
+                const int64_t yi = (!zc && py < Hp) ? pad_map(py - G.p, G.h, G.pad_mode) : -1;
+                unsigned short v[8];
+#pragma unroll
+                for (int cc = 0; cc < 8; ++cc) {
+                    const int c = c0 + cc;
+                    unsigned short e = 0;
+                    if (!zc && c < G.C && py < Hp)
+                        e = (yi < 0 || xi < 0) ? padv : xb[((int64_t)c * G.h + yi) * G.w + xi];
+                    v[cc] = e;
+                }
+                psb[pr * CB_PP + pc] = cm_u4{v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
+                                             v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16)};
+            }
+        }
+        // ---- stage the weights of taps (o, t), 8 channels, as 3 bf16 parts ----------------
+        for (int e = tid; e < CM_O * 8; e += CM_THREADS) {
+            const int o = e >> 3, t = e & 7, og = o0 + o;
+            unsigned short h[8], m[8], l[8];
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) {
+                const int c = c0 + cc;
+                const float wf = (t < 7 && og < G.O && c < G.C) ? kern[((int64_t)og * G.C + c) * 7 + t] : 0.f;
+                const __bf16 bh = (__bf16)wf;
+                const float r1 = wf - (float)bh;
+                const __bf16 bm = (__bf16)r1;
+                const __bf16 bl = (__bf16)(r1 - (float)bm);
+                h[cc] = __builtin_bit_cast(unsigned short, bh);
+                m[cc] = __builtin_bit_cast(unsigned short, bm);
+                l[cc] = __builtin_bit_cast(unsigned short, bl);
+            }
+            const int kb = t >> 2, g = t & 3;
+            auto pk = [](const unsigned short* u) {
+                return cm_u4{u[0] | ((unsigned)u[1] << 16), u[2] | ((unsigned)u[3] << 16),
+                             u[4] | ((unsigned)u[5] << 16), u[6] | ((unsigned)u[7] << 16)};
+            };
+            wsb[((0 * 2 + kb) * CM_O + o) * 4 + g] = pk(h);
+            wsb[((1 * 2 + kb) * CM_O + o) * 4 + g] = pk(m);
+            wsb[((2 * 2 + kb) * CM_O + o) * 4 + g] = pk(l);
+        }
+        __syncthreads();
+        // ---- 2 k blocks x 4 column tiles x 3 weight parts x NOT channel tiles -------------
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            cm_b8 bf[4];
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt)
+                bf[qt] = __builtin_bit_cast(cm_b8, psb[pidx[kb] < 0 ? CB_PSZ - 1 : pidx[kb] + qt * 16]);
+#pragma unroll
+            for (int pt = 0; pt < 3; ++pt) {
+#pragma unroll
+                for (int ot = 0; ot < NOT; ++ot) {
+                    const cm_b8 af = __builtin_bit_cast(cm_b8, wsb[((pt * 2 + kb) * CM_O + ot * 16 + li) * 4 + lg]);
+#pragma unroll
+                    for (int qt = 0; qt < 4; ++qt)
+                        acc[ot][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[qt], acc[ot][qt], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    if (r >= G.ho) return;
+    Tout* yb = y + b * (int64_t)G.O * G.ho * G.wo;
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int o = o0 + ot * 16 + lg * 4 + v;
+            if (o >= G.O) continue;
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt) {
+                const int q = q0 + qt * 16 + li;
+                if (q >= G.wo) continue;
+                float val = acc[ot][qt][v];
+                if (G.epi.on) val = epi_apply(val, o, G.epi);
+                yb[((int64_t)o * G.ho + r) * G.wo + q] = (Tout)val;
+            }
+        }
+}
+
 // Runs the MFMA kernel when it covers the call and pays (dense radius-2, stride-1,
 // dilation-1 conv with C >= 8 and O >= 16, f32 weights); HG_EUNSUP otherwise.
 int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_dtype,
@@ -223,6 +364,22 @@ int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_
     const int64_t blocks = B * (int64_t)G.ntq * G.ntr * G.nto;
     if (blocks > INT_MAX || blocks == 0) return blocks == 0 ? HG_OK : HG_EUNSUP;
     const dim3 grid((unsigned)blocks), blk(CM_THREADS);
+    // bf16 inputs: the split-weight bf16 kernel, when the pad value is a bf16 (the padded
+    // input keeps the input's dtype, as F.pad does; anything else keeps the f32 kernel)
+    const bool bf_pad = (double)(float)(__bf16)(float)pad_value == pad_value;
+    const char* eb = getenv("HYGRID_CONV_MFMA_BF16");   // A/B switch: 0 = the f32 kernel
+    if (x_dtype == HG_BF16 && bf_pad && !(eb && eb[0] == '0') &&
+        (y_dtype == HG_BF16 || y_dtype == HG_F32)) {
+#define HG_CB_LAUNCH(TO)                                                                      \
+        if (nt == 2)                                                                          \
+            hipLaunchKernelGGL((k_hexconv_mfma_bf16<TO, 2>), grid, blk, 0, st, (const __bf16*)x, k, b, (TO*)y, G); \
+        else                                                                                  \
+            hipLaunchKernelGGL((k_hexconv_mfma_bf16<TO, 4>), grid, blk, 0, st, (const __bf16*)x, k, b, (TO*)y, G); \
+        return launch_status();
+        if (y_dtype == HG_BF16) { HG_CB_LAUNCH(__bf16) }
+        HG_CB_LAUNCH(float)
+#undef HG_CB_LAUNCH
+    }
 #define HG_CM_LAUNCH(TI, TO)                                                                  \
     if (nt == 2)                                                                              \
         hipLaunchKernelGGL((k_hexconv_mfma<TI, TO, 2>), grid, blk, 0, st, (const TI*)x, k, b, (TO*)y, G); \

@@ -34,17 +34,21 @@ constexpr int FU_OWN = FU_OWN_;       // owned columns per 128-column window
 #ifndef FU_RB_PYR_
 #define FU_RB_PYR_ 60                 // MD 3 / 4: input rows per band (30 output rows)
 #endif
+#ifndef FU_RB_RT_
+#define FU_RB_RT_ 30                  // MD 2: rows per band (66 -> 30: 0.321 -> 0.307 ms, r03 A/B)
+#endif
 constexpr int FU_RB = FU_RB_;
 constexpr int FU_RB_CONV = FU_RB_CONV_;
 constexpr int FU_RB_PYR = FU_RB_PYR_;
-constexpr int FU_LUT = (FU_RB > FU_RB_CONV ? (FU_RB > FU_RB_PYR ? FU_RB : FU_RB_PYR)
-                                           : (FU_RB_CONV > FU_RB_PYR ? FU_RB_CONV : FU_RB_PYR)) + 2;
+constexpr int FU_RB_RT = FU_RB_RT_;
+constexpr int fu_max(int a, int b) { return a > b ? a : b; }
+constexpr int FU_LUT = fu_max(fu_max(FU_RB, FU_RB_CONV), fu_max(FU_RB_PYR, FU_RB_RT)) + 2;
 // the one definition of a mode's band length, used by the kernel and the host launchers
 __host__ __device__ constexpr int fu_rb(int md) {
-    return md == 1 ? FU_RB_CONV : (md >= 3 ? FU_RB_PYR : FU_RB);
+    return md == 1 ? FU_RB_CONV : (md >= 3 ? FU_RB_PYR : (md == 2 ? FU_RB_RT : FU_RB));
 }
-static_assert(FU_RB % 6 == 0 && FU_RB_CONV % 6 == 0 && FU_RB_PYR % 6 == 0 && FU_RB > 0 &&
-              FU_RB_CONV > 0 && FU_RB_PYR > 0,
+static_assert(FU_RB % 6 == 0 && FU_RB_CONV % 6 == 0 && FU_RB_PYR % 6 == 0 && FU_RB_RT % 6 == 0 &&
+              FU_RB > 0 && FU_RB_CONV > 0 && FU_RB_PYR > 0 && FU_RB_RT > 0,
               "bands are whole 6-step blocks (ring slots x row parities), even-aligned");
 static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
               "owned columns are whole lanes with a halo of >= 1 lane on each side");
@@ -104,6 +108,16 @@ static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
 #ifndef FU_ONE_CLASS
 #define FU_ONE_CLASS 0                // ISA inspection: instantiate only the (CD 1, RC 1) loop
 #endif
+#ifndef FU_VPK
+#define FU_VPK 1                      // PK: the r2h vertical blend as v_pk_mul/fma_f32 on the
+                                      // (even, odd) rect pair, row weights broadcast by op_sel
+#endif
+#ifndef FU_ODPP
+#define FU_ODPP 1                     // MD 0: the h2r neighbour term as one v_fmac_f32_dpp
+#endif
+// (Round 3 also measured the stencil's shifted u pairs exchanged through a per-wave LDS row
+// instead of DPP moves + pair copies: 6 fewer DPP and 6 fewer moves per step, but 130-136
+// VGPRs (3 waves per SIMD) or scratch spills at a 128 cap, 1.6-2.2 % slower)
 
 struct FusedGeom {
     int64_t B;
@@ -214,6 +228,56 @@ __device__ __forceinline__ fu_f2 fu_pfma_b(fu_f2 wp, fu_f2 a, fu_f2 bp) {
     return d;
 }
 #undef FU_PFMAB_
+// d = w[H] * a (packed multiply, weight half H broadcast; VGPR weight pair)
+template <int H>
+__device__ __forceinline__ fu_f2 fu_pmul(fu_f2 wp, fu_f2 a) {
+    fu_f2 d;
+    if constexpr (H) asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]" : "=v"(d) : "v"(wp), "v"(a));
+    else asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(d) : "v"(wp), "v"(a));
+    return d;
+}
+// The folded same-size h2r of three conv-row pairs z_o = (ze, zo) (MD 0, O = 3) as one asm
+// block: the three lane-local FMAs first, then the three neighbour terms as v_fmac_f32_dpp
+// (DPP on src0, 0 past the wave edge = f_next / f_prev), so every DPP source was written
+// >= 3 VALU instructions earlier (a DPP read needs 2 wait states after a VALU write, and the
+// hazard recognizer does not look inside an inline-asm consumer).
+//   even row: oe = c13 * zo + ze,  oo = zo + next(ze) * wn
+//   odd row:  oo = c13 * ze + zo,  oe = ze + prev(zo) * wp
+// Bit-identical to fmaf(c13, zo, ze) / fmaf(wn, f_next(ze), zo) (products commute).
+__device__ __forceinline__ void fu_h2r3_even(float& e0, float& o0, float& e1, float& o1,
+                                             float& e2, float& o2, float c13, float wn) {
+    float a0, a1, a2;
+    asm("v_fma_f32 %0, %9, %4, %3\n\t"
+        "v_fma_f32 %1, %9, %6, %5\n\t"
+        "v_fma_f32 %2, %9, %8, %7\n\t"
+        "v_fmac_f32_dpp %4, %3, %10 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f32_dpp %6, %5, %10 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f32_dpp %8, %7, %10 wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "+v"(e0), "+v"(o0), "+v"(e1), "+v"(o1), "+v"(e2),
+          "+v"(o2)
+        : "v"(c13), "v"(wn));
+    e0 = a0; e1 = a1; e2 = a2;
+}
+__device__ __forceinline__ void fu_h2r3_odd(float& e0, float& o0, float& e1, float& o1,
+                                            float& e2, float& o2, float c13, float wp) {
+    float a0, a1, a2;
+    asm("v_fma_f32 %0, %9, %3, %4\n\t"
+        "v_fma_f32 %1, %9, %5, %6\n\t"
+        "v_fma_f32 %2, %9, %7, %8\n\t"
+        "v_fmac_f32_dpp %3, %4, %10 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f32_dpp %5, %6, %10 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_fmac_f32_dpp %7, %8, %10 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "+v"(e0), "+v"(o0), "+v"(e1), "+v"(o1), "+v"(e2),
+          "+v"(o2)
+        : "v"(c13), "v"(wp));
+    o0 = a0; o1 = a1; o2 = a2;
+}
+template <typename T>
+__device__ __forceinline__ fu_f2 fu_unpack2(typename RawOf<T>::type r, unsigned hi16) {
+    float e, o;
+    fu_unpack<T>(r, e, o, hi16);
+    return fu_f2{e, o};
+}
 __host__ __device__ constexpr int fu_mod(int a, int m) { return ((a % m) + m) % m; }
 // compile-time loop: f(IC<B>{}), f(IC<B+1>{}), ..., f(IC<E-1>{})
 template <int B, int E, typename F>
@@ -247,6 +311,7 @@ void k_fused(const Tin* __restrict__ x,
     constexpr int PD = FU_PD;
     constexpr bool PYR = MD >= 3;                 // hex-pyramid level (hexresize output stage)
     constexpr bool UIN = MD == 1 || MD == 4;      // u rows = input rows (no r2h)
+    constexpr bool VPK = FU_VPK && FU_PK && MD != 2 && !UIN;
     static_assert(PD >= 1 && PD <= 5, "raw ring: rows a2+2 .. a2+1+PD in flight in 6 slots");
     using Raw = typename RawOf<Tin>::type;
 
@@ -439,7 +504,7 @@ void k_fused(const Tin* __restrict__ x,
         constexpr int RC = decltype(RCc)::value;
         // ---- state -----------------------------------------------------------------
         Raw raw[6][C];                      // rect rows in flight, slot (row - s0) % 6
-        float XE[3][C], XO[3][C];           // rect rows as f32, slot (row - s0) % 3
+        fu_f2 XP[3][C];                     // rect rows as f32 (even, odd) pairs, slot (row - s0) % 3
         float ZE[3][O], ZO[3][O];           // conv rows being accumulated, slot (row - s0) % 3
         constexpr bool PK = FU_PK && MD != 2;
         static_assert(PK || !PYR, "the pyramid modes use the packed stencil");
@@ -455,7 +520,7 @@ void k_fused(const Tin* __restrict__ x,
         auto convert = [&](auto RSc, auto XSc) {
             constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
     #pragma unroll
-            for (int c = 0; c < C; ++c) fu_unpack<Tin>(raw[RS][c], XE[XS][c], XO[XS][c], hi16);
+            for (int c = 0; c < C; ++c) XP[XS][c] = fu_unpack2<Tin>(raw[RS][c], hi16);
         };
 
         // u row r (= s0 + PH + 1) from rect rows r-1, r, r+1 (ring slots PH, PH+1, PH+2
@@ -468,26 +533,45 @@ void k_fused(const Tin* __restrict__ x,
             constexpr int PB = fu_mod(PH, 2);       // parity of conv row r-1 (and r+1)
             constexpr int PC = 1 - PB;              // parity of conv row r
             float ue[C], uo[C];
-            if constexpr (UIN) {                    // u = input row, 0 outside (padding 1, value 0)
+            if constexpr (UIN && RC == 1) {         // interior band and window: no padding
+    #pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    ue[c] = XP[S1][c].x;
+                    uo[c] = XP[S1][c].y;
+                }
+            } else if constexpr (UIN) {             // u = input row, 0 outside (padding 1, value 0)
                 const bool in_ = colin && L.y != 0.f;
     #pragma unroll
                 for (int c = 0; c < C; ++c) {
-                    ue[c] = in_ ? XE[S1][c] : 0.f;
-                    uo[c] = in_ ? XO[S1][c] : 0.f;
+                    ue[c] = in_ ? XP[S1][c].x : 0.f;
+                    uo[c] = in_ ? XP[S1][c].y : 0.f;
                 }
             } else
     #pragma unroll
             for (int c = 0; c < C; ++c) {
                 float ve, vo;
-                if constexpr (RC == 1) {            // rect rows r-1, r
-                    ve = fmaf(L.y, XE[S1][c], L.x * XE[S0][c]);
-                    vo = fmaf(L.y, XO[S1][c], L.x * XO[S0][c]);
+                if constexpr (VPK) {                // the same products and sums, packed
+                    const fu_f2 Lxy = {L.x, L.y}, Lzw = {L.z, L.w};
+                    fu_f2 V;
+                    if constexpr (RC == 1) {
+                        V = fu_pfma<1, false>(Lxy, XP[S1][c], fu_pmul<0>(Lxy, XP[S0][c]));
+                    } else if constexpr (RC == 2) {
+                        V = fu_pfma<0, false>(Lzw, XP[S2][c], fu_pmul<1>(Lxy, XP[S1][c]));
+                    } else {
+                        V = fu_pfma<0, false>(Lzw, XP[S2][c],
+                                              fu_pfma<1, false>(Lxy, XP[S1][c], fu_pmul<0>(Lxy, XP[S0][c])));
+                    }
+                    ve = V.x;
+                    vo = V.y;
+                } else if constexpr (RC == 1) {     // rect rows r-1, r
+                    ve = fmaf(L.y, XP[S1][c].x, L.x * XP[S0][c].x);
+                    vo = fmaf(L.y, XP[S1][c].y, L.x * XP[S0][c].y);
                 } else if constexpr (RC == 2) {     // rect rows r, r+1
-                    ve = fmaf(L.z, XE[S2][c], L.y * XE[S1][c]);
-                    vo = fmaf(L.z, XO[S2][c], L.y * XO[S1][c]);
+                    ve = fmaf(L.z, XP[S2][c].x, L.y * XP[S1][c].x);
+                    vo = fmaf(L.z, XP[S2][c].y, L.y * XP[S1][c].y);
                 } else {
-                    ve = fmaf(L.z, XE[S2][c], fmaf(L.y, XE[S1][c], L.x * XE[S0][c]));
-                    vo = fmaf(L.z, XO[S2][c], fmaf(L.y, XO[S1][c], L.x * XO[S0][c]));
+                    ve = fmaf(L.z, XP[S2][c].x, fmaf(L.y, XP[S1][c].x, L.x * XP[S0][c].x));
+                    vo = fmaf(L.z, XP[S2][c].y, fmaf(L.y, XP[S1][c].y, L.x * XP[S0][c].y));
                 }
                 if constexpr (CD == 1) {            // taps q-1, q
                     ue[c] = fmaf(we[1], ve, we[0] * f_prev(vo));
@@ -670,6 +754,16 @@ void k_fused(const Tin* __restrict__ x,
                 return;
             }
             const unsigned so = FU_NOMEM ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
+            if constexpr (FU_ODPP && FOLD && PK && O == 3 && !STAGE) {
+                float e0 = ZP[S0][0].x, o0 = ZP[S0][0].y, e1 = ZP[S0][1].x, o1 = ZP[S0][1].y;
+                float e2 = ZP[S0][2].x, o2 = ZP[S0][2].y;
+                if constexpr ((PH & 1) == 0) fu_h2r3_even(e0, o0, e1, o1, e2, o2, c13, wn_f);
+                else fu_h2r3_odd(e0, o0, e1, o1, e2, o2, c13, wp_f);
+                fu_store<Tout>(e0, o0, yrs, yoff, so);
+                fu_store<Tout>(e1, o1, yrs, yoff, so + yplane);
+                fu_store<Tout>(e2, o2, yrs, yoff, so + 2 * yplane);
+                return;
+            }
     #pragma unroll
             for (int o = 0; o < O; ++o) {
                 const float ze = PK ? ZP[S0][o].x : ZE[S0][o], zo = PK ? ZP[S0][o].y : ZO[S0][o];
@@ -752,9 +846,9 @@ void k_fused(const Tin* __restrict__ x,
             }
     #pragma unroll
             for (int c = 0; c < C; ++c) {
-                fu_unpack<Tin>(t0[c], XE[1][c], XO[1][c], hi16);   // row s0-2 -> slot 1
-                fu_unpack<Tin>(t1[c], XE[2][c], XO[2][c], hi16);   // row s0-1 -> slot 2
-                fu_unpack<Tin>(t2[c], XE[0][c], XO[0][c], hi16);   // row s0   -> slot 0
+                XP[1][c] = fu_unpack2<Tin>(t0[c], hi16);   // row s0-2 -> slot 1
+                XP[2][c] = fu_unpack2<Tin>(t1[c], hi16);   // row s0-1 -> slot 2
+                XP[0][c] = fu_unpack2<Tin>(t2[c], hi16);   // row s0   -> slot 0
             }
         }
         urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});   // u row s0-1: above only
@@ -826,7 +920,11 @@ void k_fused(const Tin* __restrict__ x,
     };
     if constexpr (UIN) {
         (void)cd; (void)rc;
-        run(IC<0>{}, IC<0>{});
+        // every u row of the band (s0 - 1 .. s1) and every lane's columns inside the input:
+        // the padding selects drop out (RC 1 marks that loop for the u = input modes)
+        const bool inner = s0 >= 1 && s1 + 1 <= F.h && __builtin_amdgcn_ballot_w64(!colin) == 0;
+        if (inner) run(IC<0>{}, IC<1>{});
+        else run(IC<0>{}, IC<0>{});
     } else {
         // the common classes get their own loop; mixed windows / bands run the generic one
         if (FU_ONE_CLASS) run(IC<1>{}, IC<1>{});

@@ -484,6 +484,11 @@ static int resample(const void* src, void* dst, int sdt, int ddt, int64_t planes
     if (planes * h1 * w1 > 0 && (!dst || (h * w > 0 && !src))) return HG_EINVAL;
     const Geom g = geom_for(OP, h, w, h1, w1);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (OP == OP_R2H && (interp == HG_NEAREST || (interp == HG_LINEAR && !acc_is_double(sdt, ddt)))) {
+        // ~2x downsampling lattices (ConvertToHexagon, the demo): row-streaming kernel
+        const int rc = down_try(src, dst, sdt, ddt, planes, h, w, h1, w1, interp, s);
+        if (rc != HG_EUNSUP) return rc;
+    }
     if (interp == HG_NEAREST) {
         if (sdt != ddt) return HG_EDTYPE;
         switch (dtype_size(sdt)) {
@@ -526,6 +531,25 @@ int hg_hexresize(const void* src, void* dst, int sdt, int ddt, int64_t planes, i
                  int64_t w, int64_t h1, int64_t w1, int interp, void* stream) {
     return hg::resample<hg::OP_RESIZE>(src, dst, sdt, ddt, planes, h, w, h1, w1, interp,
                                        stream);
+}
+
+int hg_resample_kernel(int op, int sdt, int ddt, int64_t planes, int64_t h, int64_t w,
+                       int64_t h1, int64_t w1, int interp) {
+    // the dispatch of hg::resample, without launching
+    int st = hg::check_sizes(planes, h, w, h1, w1);
+    if (st) return st;
+    if (op != HG_OP_RECT_TO_HEX && op != HG_OP_HEX_TO_RECT && op != HG_OP_HEXRESIZE) return HG_EINVAL;
+    if (interp == HG_NEAREST && sdt != ddt) return HG_EDTYPE;
+    if (interp != HG_NEAREST && interp != HG_LINEAR) return HG_EINVAL;
+    const bool dbl = interp == HG_LINEAR && hg::acc_is_double(sdt, ddt);
+    if (op == HG_OP_RECT_TO_HEX && !dbl &&
+        hg::down_try(nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, interp, nullptr, true) == HG_OK)
+        return HG_KERNEL_DOWN;
+    if (interp == HG_NEAREST) return HG_KERNEL_NEAREST;
+    if (!dbl && op != HG_OP_HEXRESIZE &&
+        hg::stream_try(op, nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, nullptr, true) == HG_OK)
+        return HG_KERNEL_STREAM;
+    return HG_KERNEL_GENERAL;
 }
 
 int hg_lattice_maps(int op, int64_t h, int64_t w, int64_t h1, int64_t w1, int32_t* imaps,

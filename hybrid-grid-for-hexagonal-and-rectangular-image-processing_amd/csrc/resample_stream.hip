@@ -494,7 +494,7 @@ static bool h2r_exact(const Geom& g, float tri[2][3]) {
 }
 
 int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h,
-               int64_t w, int64_t h1, int64_t w1, hipStream_t st) {
+               int64_t w, int64_t h1, int64_t w1, hipStream_t st, bool dry) {
     if (const char* e = getenv("HYGRID_STREAM")) {    // A/B switch: 0 = general kernels only
         if (e[0] == '0') return HG_EUNSUP;
     }
@@ -520,6 +520,7 @@ int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t pla
     S.nwin = (int)((w1 + 64 * cpl - 1) / (64 * cpl));
     S.rb = op == HG_OP_RECT_TO_HEX ? ST_RB_R2H : ST_RB_H2R;
     S.nband = (int)((h1 + S.rb - 1) / S.rb);
+    if (dry) return HG_OK;
     if (sdt == HG_BF16 && ddt == HG_BF16) return stream_launch<__bf16, __bf16>(op, src, dst, S, st);
     if (sdt == HG_F16 && ddt == HG_F16) return stream_launch<_Float16, _Float16>(op, src, dst, S, st);
     if (sdt == HG_F32 && ddt == HG_F32) return stream_launch<float, float>(op, src, dst, S, st);

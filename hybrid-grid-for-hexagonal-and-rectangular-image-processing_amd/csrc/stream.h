@@ -9,7 +9,13 @@ namespace hg {
 // Runs the streaming kernel if the call is in its domain (r2h with a near-identity
 // lattice, h2r at the same size; 16/32-bit float in and out; widths a multiple of 4);
 // returns HG_EUNSUP (nothing launched) otherwise.  Bit-identical to the general kernels.
+// dry: only the domain check (HG_OK = the kernel would run), nothing launched.
 int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h,
-               int64_t w, int64_t h1, int64_t w1, hipStream_t st);
+               int64_t w, int64_t h1, int64_t w1, hipStream_t st, bool dry = false);
+
+// ~2x downsampling rect->hex (ConvertToHexagon's (h//2, w//2) 'nearest' on 8/16-bit data, the
+// demo's bilinear on bf16/f16; resample_down.hip); HG_EUNSUP (nothing launched) otherwise.
+int down_try(const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h, int64_t w,
+             int64_t h1, int64_t w1, int interp, hipStream_t st, bool dry = false);
 
 }  // namespace hg

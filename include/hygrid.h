@@ -104,6 +104,16 @@ int hg_hexresize(const void* src, void* dst, int src_dtype, int dst_dtype, int64
 int hg_resample_backward(int op, const void* gy, void* dx, int acc_dtype, int64_t planes,
                          int64_t h, int64_t w, int64_t h1, int64_t w1, int interp, void* stream);
 
+/* Which kernel hg_rect_to_hex / hg_hex_to_rect / hg_hexresize would run for this call
+ * (nothing is launched): HG_KERNEL_GENERAL (k_resample_lds / k_resample_direct),
+ * HG_KERNEL_NEAREST (k_resample_nearest), HG_KERNEL_STREAM (near-identity row streaming,
+ * resample_stream.hip), HG_KERNEL_DOWN (~2x downsampling rect->hex, resample_down.hip), or a
+ * negative status.  Introspection for tests and tools; the reference has no counterpart. */
+enum hg_kernel { HG_KERNEL_GENERAL = 0, HG_KERNEL_NEAREST = 1, HG_KERNEL_STREAM = 2,
+                 HG_KERNEL_DOWN = 3 };
+int hg_resample_kernel(int op, int src_dtype, int dst_dtype, int64_t planes, int64_t h, int64_t w,
+                       int64_t h1, int64_t w1, int interp);
+
 /* Integer lattice maps (and fp64 coefficients) of one resample, for parity tests.
  * imaps: int32 [5][h1][w1] = i_n, j_n, up_down_flag, valid bitmask (bit k-1 =
  *        valid_indices_k), nearest argmin — the locals of the reference function

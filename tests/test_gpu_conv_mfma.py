@@ -123,3 +123,82 @@ def test_mfma_conv_nan_positions_match_generic():
     ref = _generic(ops.hexconv2d, x, k, b, 1, 2, padding=1, out_dtype=torch.float32)
     assert torch.equal(torch.isnan(y), torch.isnan(ref))
     assert torch.equal(torch.isinf(y), torch.isinf(ref))
+
+
+# ---- bf16 inputs: the split-weight bf16 MFMA kernel (k_hexconv_mfma_bf16) ----------------
+
+def _bf16_input(shape, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.rand(shape, generator=g, device=DEV) - 0.5).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("pad", [0, 1, 2])
+@pytest.mark.parametrize("off", [0, 1])
+def test_mfma_bf16_conv_vs_oracle(case, pad, off):
+    """bf16 input (exact in fp64), fp32 output: W = Wh + Wm + Wl in bf16 parts on
+    v_mfma_f32_16x16x32_bf16 must keep the fp32 kernel's 1e-5 against the fp64 oracle."""
+    B, C, O_, h, w = case
+    k, b = _weights(O_, C, h * 13 + w + pad)
+    x = _bf16_input((B, C, h, w), h + w * 3 + off)
+    y = ops.hexconv2d(x, k, b, off, 2, padding=pad, out_dtype=torch.float32).cpu().numpy()
+    ref = O.hexconv2d(x.double().cpu().numpy(), k.cpu().double().numpy(),
+                      b.cpu().double().numpy(), off, 2, padding=pad)
+    scale = max(np.abs(ref).max(), 1e-30)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5 * scale)
+
+
+@pytest.mark.parametrize("mode,pv", [("constant", 0.5), ("constant", 0.3), ("reflect", 0.0),
+                                     ("replicate", 0.0), ("circular", 0.0)])
+def test_mfma_bf16_pad_modes_vs_oracle(mode, pv):
+    """A pad value that is not a bf16 (0.3) keeps the f32 kernel; either way 1e-5."""
+    B, C, O_, h, w = 1, 16, 32, 14, 40
+    k, b = _weights(O_, C, 7)
+    x = _bf16_input((B, C, h, w), 5)
+    y = ops.hexconv2d(x, k, b, 0, 2, padding=1, padding_mode=mode, padding_value=pv,
+                      out_dtype=torch.float32).cpu().numpy()
+    ref = O.hexconv2d(x.double().cpu().numpy(), k.cpu().double().numpy(),
+                      b.cpu().double().numpy(), 0, 2, padding=1, padding_mode=mode,
+                      padding_value=pv)
+    scale = max(np.abs(ref).max(), 1e-30)
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5 * scale)
+
+
+def test_mfma_bf16_vs_f32_kernel_and_weight_split():
+    """The bf16 kernel against the f32 MFMA kernel (HYGRID_CONV_MFMA_BF16=0) at the wide
+    bench shape's channel counts, with weights whose bf16 split needs all three parts."""
+    B, C, O_, h, w = 1, 64, 64, 24, 150
+    g = torch.Generator().manual_seed(11)
+    k = ((torch.rand((O_, C, 1, 7), generator=g) - 0.5) * 0.3 + 1e-3).to(DEV)
+    b = (torch.rand((O_,), generator=g) - 0.5).to(DEV)
+    x = _bf16_input((B, C, h, w), 3)
+    y = ops.hexconv2d(x, k, b, 0, 2, padding=1, out_dtype=torch.float32)
+    old = os.environ.get("HYGRID_CONV_MFMA_BF16")
+    os.environ["HYGRID_CONV_MFMA_BF16"] = "0"
+    try:
+        ref = ops.hexconv2d(x, k, b, 0, 2, padding=1, out_dtype=torch.float32)
+        torch.cuda.synchronize()
+    finally:
+        if old is None:
+            del os.environ["HYGRID_CONV_MFMA_BF16"]
+        else:
+            os.environ["HYGRID_CONV_MFMA_BF16"] = old
+    assert not torch.equal(y, ref)   # a different kernel (summation order) ran
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+
+
+def test_mfma_bf16_nan_positions_match_generic():
+    B, C, O_, h, w = 1, 16, 16, 20, 70
+    k, b = _weights(O_, C, 4)
+    x = _bf16_input((B, C, h, w), 8)
+    x[0, 3, 0, 5] = float("nan")
+    x[0, 7, 19, 69] = float("inf")
+    x[0, 9, 10, 30] = float("-inf")
+    y = ops.hexconv2d(x, k, b, 1, 2, padding=1, out_dtype=torch.float32)
+    ref = _generic(ops.hexconv2d, x, k, b, 1, 2, padding=1, out_dtype=torch.float32)
+    # the same non-finite positions; an infinite input times a weight part that is exactly 0
+    # (a weight with fewer than 17 significant bits) is NaN where one fp32 product is +-Inf
+    assert torch.equal(~torch.isfinite(y), ~torch.isfinite(ref))
+    assert torch.equal(torch.isnan(ref) & ~torch.isnan(y), torch.zeros_like(y, dtype=torch.bool))
+    fin = torch.isfinite(ref)
+    torch.testing.assert_close(y[fin], ref[fin], rtol=1e-5, atol=1e-5 * float(ref[fin].abs().max()))

@@ -1,12 +1,15 @@
 """Interleaved A/B timing of fused-kernel variants in ONE process (same GPU, same clocks):
-each round launches every variant library once on the same device buffers; reports the
-median / min per-launch time over the rounds (HIP events on the launch stream).
+each round launches every variant library three times back to back (the last launch is
+timed) in a shuffled order on the same device buffers; reports the median / min per-launch
+time over the rounds (HIP events on the launch stream) and the median of the per-round
+ratios to the first variant named.
 
 usage: python tools/ab_fused.py [rounds] name1 name2 ...   (name 'base' = the in-tree lib;
        others = HyGrid/_lib/variants/libhygrid_<name>.so); env AB_BATCH (default 128).
 """
 import ctypes
 import os
+import random
 import statistics
 import sys
 
@@ -44,25 +47,35 @@ def main():
     args = lambda: (x.data_ptr(), k.data_ptr(), b.data_ptr(), y.data_ptr(), 7, 7, B, C, C, H, W,
                     H, W, H, W, 1, 1, 0, 0.0, st.cuda_stream)
     times = {n: [] for n in names}
+    ratios = {n: [] for n in names}
     sums = {}
+    rng = random.Random(7)
     for r in range(rounds + 1):
-        for n, f in fns.items():
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            rc = f(*args())
-            e1.record()
-            if rc != 0:
-                raise SystemExit(f"{n}: status {rc}")
+        order = list(fns.items())
+        rng.shuffle(order)               # no fixed position in the round (clock / heat drift)
+        rt = {}
+        for n, f in order:
+            for rep in range(3):         # back-to-back launches; the last one is timed
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rc = f(*args())
+                e1.record()
+                if rc != 0:
+                    raise SystemExit(f"{n}: status {rc}")
             e1.synchronize()
-            if r > 0:
-                times[n].append(e0.elapsed_time(e1))
+            rt[n] = e0.elapsed_time(e1)
             if r == rounds:
                 sums[n] = float(y.float().sum().item())
+        if r > 0:
+            for n in names:
+                times[n].append(rt[n])
+                ratios[n].append(rt[n] / rt[names[0]])
     alg = 2.0 * B * C * H * W * 2
     for n in names:
         t = times[n]
         print(f"{n:14s} median {statistics.median(t):.4f} ms  min {min(t):.4f} ms  "
-              f"{alg / statistics.median(t) / 1e6:.0f} GB/s  checksum {sums[n]:.6e}", flush=True)
+              f"{alg / statistics.median(t) / 1e6:.0f} GB/s  vs {names[0]} {statistics.median(ratios[n]):.4f}  "
+              f"checksum {sums[n]:.6e}", flush=True)
 
 
 if __name__ == "__main__":

@@ -1,9 +1,11 @@
 """Interleaved in-process A/B timing of library variants for the unfused hot-path operators
-(one process, same device buffers, HIP events on the launch stream; median / min per launch).
+(one process, same device buffers, HIP events on the launch stream; each round runs every
+variant three times back to back in a shuffled order and times the last launch; median /
+min per launch and the median per-round ratio to the first variant named).
 
 usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
-  OP: r2h | h2r | conv | r2h32 | h2r32 | pyr | pyrfr | pyr1   (bf16 4K b128 for r2h/h2r/conv;
-      fp32 1080p b32 for r2h32/h2r32; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K from a
+  OP: r2h | h2r | conv | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1   (bf16 4K b128 for
+      r2h/h2r/conv; fp32 1080p b32 for r2h32/h2r32 and rt, the fused round trip; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K from a
       hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K)
   name 'base' = the in-tree library; others = HyGrid/_lib/variants/libhygrid_<name>.so;
   'name%VAR=VAL' runs that library with the environment variable VAR=VAL set around its calls
@@ -11,6 +13,7 @@ usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
 """
 import ctypes
 import os
+import random
 import statistics
 import sys
 
@@ -40,7 +43,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(2)
     if op in ("r2h", "h2r", "conv"):
         B, C, H, W, t = 128, 3, 2160, 3840, torch.bfloat16
-    elif op in ("r2h32", "h2r32"):
+    elif op in ("r2h32", "h2r32", "rt"):
         B, C, H, W, t = 32, 3, 1080, 1920, torch.float32
     elif op == "pyr1":
         B, C, H, W, t = 8, 3, 2160, 3840, torch.float16
@@ -65,6 +68,10 @@ def main():
             f = lib.hg_hex_to_rect
             f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_int, _vp]
             return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, H, W, 1, s)
+        if op == "rt":
+            f = lib.hg_pipeline_r2h_h2r
+            f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_vp]
+            return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, H, W, s)
         if op == "conv":
             f = lib.hg_hexconv2d
             f.argtypes = [_vp] * 4 + [_int] * 3 + [_i64] * 5 + [_int] * 7 + [_dbl, _vp]
@@ -76,30 +83,40 @@ def main():
                  taps.data_ptr(), None, 0, 1 if op == "pyrfr" else 0, s)
 
     times = {n: [] for n in names}
+    ratios = {n: [] for n in names}
     sums = {}
+    rng = random.Random(7)
     for r in range(rounds + 1):
-        for n, lib in libs.items():
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        order = list(libs.items())
+        rng.shuffle(order)               # no fixed position in the round (clock / heat drift)
+        rt = {}
+        for n, lib in order:
             env = n.split("%")[1].split("=") if "%" in n else None
             if env:
                 os.environ[env[0]] = env[1]
-            e0.record()
-            rc = call(lib)
-            e1.record()
+            for rep in range(3):         # back-to-back launches; the last one is timed
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rc = call(lib)
+                e1.record()
+                if rc != 0:
+                    raise SystemExit(f"{n}: status {rc}")
             if env:
                 del os.environ[env[0]]
-            if rc != 0:
-                raise SystemExit(f"{n}: status {rc}")
             e1.synchronize()
-            if r > 0:
-                times[n].append(e0.elapsed_time(e1))
+            rt[n] = e0.elapsed_time(e1)
             if r == rounds:
                 sums[n] = float(y.double().sum().item())
+        if r > 0:
+            for n in names:
+                times[n].append(rt[n])
+                ratios[n].append(rt[n] / rt[names[0]])
     alg = x.numel() * x.element_size() + y.numel() * y.element_size()
     for n in names:
         tm = times[n]
         print(f"{op:6s} {n:14s} median {statistics.median(tm):.4f} ms  min {min(tm):.4f} ms  "
-              f"{alg / statistics.median(tm) / 1e6:.0f} GB/s  checksum {sums[n]:.9e}", flush=True)
+              f"{alg / statistics.median(tm) / 1e6:.0f} GB/s  vs {names[0]} "
+              f"{statistics.median(ratios[n]):.4f}  checksum {sums[n]:.9e}", flush=True)
 
 
 if __name__ == "__main__":
