@@ -112,6 +112,11 @@ static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
 #define FU_VPK 1                      // PK: the r2h vertical blend as v_pk_mul/fma_f32 on the
                                       // (even, odd) rect pair, row weights broadcast by op_sel
 #endif
+#ifndef FU_PLDS
+#define FU_PLDS 1                     // MD 3 / 4: the triangle vertices read from the wave's two
+                                      // conv rows in LDS (3 ds_read_b32 per channel at per-lane
+                                      // addresses) instead of 5 DPP moves + 9 selects per channel
+#endif
 #ifndef FU_ODPP
 #define FU_ODPP 1                     // MD 0: the h2r neighbour term as one v_fmac_f32_dpp
 #endif
@@ -325,9 +330,18 @@ void k_fused(const Tin* __restrict__ x,
     // per-wave u-row table {a, b, c, -}: u[r] = a*x[r-1] + b*x[r] + c*x[r+1]
     __shared__ float4 lut_all[GW][FU_LUT];
     __shared__ unsigned stg[STAGE ? 2 : 1][STAGE ? 6 : 1][STAGE ? O : 1][STAGE ? GDW + 4 : 1];
+    // PLDS: the two conv rows an output row reads, per wave: [row][channel][col], cols
+    // 0..127 of the window + a zero at 128 (vertices outside the raster) and a pad
+    constexpr bool PLDS = FU_PLDS && PYR;
+    constexpr int ZW = 130;
+    __shared__ float zl_all[PLDS ? GW : 1][PLDS ? 2 * O * ZW : 1];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4* lut = lut_all[wslot];
+    float* zl = zl_all[PLDS ? wslot : 0];
+    if constexpr (PLDS) {
+        if (lane < 2 * O) zl[lane * ZW + 128] = 0.f;   // the zero vertex of every row block
+    }
     const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
     const int ngrp = (F.nwin + GW - 1) / GW;
     const int grp = (int)(blk % ngrp);
@@ -717,6 +731,34 @@ void k_fused(const Tin* __restrict__ x,
             const bool v2 = flag ? (r1in && c1 >= 0 && c1 < F.w1) : (c0 + 1 >= 0 && c0 + 1 < F.w1);
             const bool v3 = r1in && c1 + 1 >= 0 && c1 + 1 < F.w1;
             const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a * yrow));
+            if constexpr (PLDS) {
+                // conv row 2a + 1 next to row 2a (written at the previous step); per-lane
+                // vertex addresses (window-local columns, clamped: halo lanes only), the
+                // zero vertex outside the raster; the same arithmetic as below
+                asm volatile("" ::: "memory");
+    #pragma unroll
+                for (int o = 0; o < O; ++o)
+                    *reinterpret_cast<fu_f2*>(&zl[(O + o) * ZW + 2 * lane]) = Z1[o];
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                const int r0b = e1 ? O * ZW : 0;
+                auto col = [&](int c) { return min(max(c - W0, 0), 127); };
+                const int a1 = v1 ? r0b + col(c0) : 128;
+                const int a2 = v2 ? (flag ? O * ZW + col(c1) : r0b + col(c0 + 1)) : 128;
+                const int a3 = v3 ? O * ZW + col(c1 + 1) : 128;
+    #pragma unroll
+                for (int o = 0; o < O; ++o) {
+                    const float q1 = zl[a1 + o * ZW], q2 = zl[a2 + o * ZW], q3 = zl[a3 + o * ZW];
+                    const float z = fmaf(wg, q3, fmaf(wb, q2, wa * q1));
+                    if constexpr (sizeof(Tout) == 2)
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, (Tout)z),
+                                                              yrs, yoff, so + o * yplane, 0);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, z), yrs, yoff,
+                                                              so + o * yplane, 0);
+                }
+                return;
+            }
     #pragma unroll
             for (int o = 0; o < O; ++o) {
                 const fu_f2 z0 = e1 ? Z1[o] : ZK[o], z1 = Z1[o];
@@ -746,8 +788,15 @@ void k_fused(const Tin* __restrict__ x,
             constexpr int S0 = PH % 3;
             if constexpr (PYR) {
                 if constexpr ((PH & 1) == 0) {      // conv row 2a: kept for the next step
+                    if constexpr (PLDS) {
+                        asm volatile("" ::: "memory");   // after the previous row's reads
     #pragma unroll
-                    for (int o = 0; o < O; ++o) ZK[o] = ZP[S0][o];
+                        for (int o = 0; o < O; ++o)
+                            *reinterpret_cast<fu_f2*>(&zl[o * ZW + 2 * lane]) = ZP[S0][o];
+                    } else {
+    #pragma unroll
+                        for (int o = 0; o < O; ++o) ZK[o] = ZP[S0][o];
+                    }
                 } else {                            // conv row 2a + 1: output row a
                     pyr_out(ZP[S0], a2 >> 1);
                 }

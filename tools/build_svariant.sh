@@ -12,7 +12,7 @@ OBJ=$PKG/build/obj
 OUT=$PKG/HyGrid/_lib/variants
 mkdir -p "$OUT" "$OBJ/variants"
 EXTRA=""
-case "$BASE" in fused|fused_conv|resample_stream) EXTRA="-fno-slp-vectorize" ;; esac
+case "$BASE" in fused|fused_conv|resample_stream|pyramid_fused|pyramid_stream) EXTRA="-fno-slp-vectorize" ;; esac
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $EXTRA "$@" \
     -I"$PKG/csrc" -c "$PKG/csrc/$BASE.hip" -o "$OBJ/variants/${BASE}_$NAME.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libhygrid_$NAME.so" \
