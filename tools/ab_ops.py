@@ -4,7 +4,7 @@ variant three times back to back in a shuffled order and times the last launch; 
 min per launch and the median per-round ratio to the first variant named).
 
 usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
-  OP: r2h | h2r | conv | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1   (bf16 4K b128 for
+  OP: r2h | h2r | conv | wide (HexConv2d 64->64, 1080p bf16 b4) | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1   (bf16 4K b128 for
       r2h/h2r/conv; fp32 1080p b32 for r2h32/h2r32 and rt, the fused round trip; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K from a
       hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K)
   name 'base' = the in-tree library; others = HyGrid/_lib/variants/libhygrid_<name>.so;
@@ -45,6 +45,8 @@ def main():
         B, C, H, W, t = 128, 3, 2160, 3840, torch.bfloat16
     elif op in ("r2h32", "h2r32", "rt"):
         B, C, H, W, t = 32, 3, 1080, 1920, torch.float32
+    elif op == "wide":
+        B, C, H, W, t = 4, 64, 1080, 1920, torch.bfloat16
     elif op == "pyr1":
         B, C, H, W, t = 8, 3, 2160, 3840, torch.float16
     else:
@@ -55,8 +57,9 @@ def main():
         taps = (torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32, device=dev) / 12).repeat(C)
     else:
         y = torch.empty_like(x)
-    k = (torch.rand((3, 21), generator=g, device=dev) - 0.5) * 0.5
-    b = torch.rand((3,), generator=g, device=dev) - 0.5
+    kc = C if op == "wide" else 3
+    k = (torch.rand((kc, 7 * kc), generator=g, device=dev) - 0.5) * (0.5 if kc == 3 else 0.05)
+    b = torch.rand((kc,), generator=g, device=dev) - 0.5
     s = st.cuda_stream
 
     def call(lib):
@@ -72,7 +75,7 @@ def main():
             f = lib.hg_pipeline_r2h_h2r
             f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_vp]
             return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, H, W, s)
-        if op == "conv":
+        if op in ("conv", "wide"):
             f = lib.hg_hexconv2d
             f.argtypes = [_vp] * 4 + [_int] * 3 + [_i64] * 5 + [_int] * 7 + [_dbl, _vp]
             return f(x.data_ptr(), k.data_ptr(), b.data_ptr(), y.data_ptr(), dt[t], _abi.HG_F32,
