@@ -24,9 +24,10 @@ constexpr int FU_HL = FU_HL_;         // halo columns on the left of a window
 constexpr int FU_OWN = FU_OWN_;       // owned columns per 128-column window
 // Output rows per band (multiple of 6), MD 0 / MD 1.  Shorter bands than the 126 of
 // round 1 measured faster (in-process A/B on 4K bf16 b128, tools/ab_fused.py /
-// tools/ab_ops.py): pipeline 3.00 -> 2.83 ms at 66, HexConv2d 3.19 -> 2.73 ms at 18.
+// tools/ab_ops.py): pipeline 3.00 -> 2.83 ms at 66 (round 2), 66 -> 42 a further -1.8 %
+// (round 3, profiles/r03/g); HexConv2d 3.19 -> 2.73 ms at 18.
 #ifndef FU_RB_
-#define FU_RB_ 66
+#define FU_RB_ 42
 #endif
 #ifndef FU_RB_CONV_
 #define FU_RB_CONV_ 18
