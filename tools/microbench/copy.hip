@@ -33,6 +33,23 @@ __global__ __launch_bounds__(256) void copy_chunk(const f4v* __restrict__ x, f4v
     }
 }
 
+// one-shot copy of T elements: U per thread (lane-contiguous), all loads before the stores
+template <typename T, int U>
+__global__ __launch_bounds__(256) void copy_el(const T* __restrict__ x, T* __restrict__ y, int64_t n) {
+    const int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x;
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * 256;
+        if (i < n) v[u] = x[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * 256;
+        if (i < n) y[i] = v[u];
+    }
+}
+
 template <typename K>
 float timeit(K k, int reps) {
     hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -61,5 +78,11 @@ int main() {
 #define CH(U, NT) rep("chunk " #U " float4/thread" #NT, timeit([&] { \
         hipLaunchKernelGGL((copy_chunk<U, NT>), dim3((unsigned)((n + 256 * U - 1) / (256 * U))), dim3(256), 0, 0, (const f4v*)x, (f4v*)y, n); }, 10));
     CH(1, false) CH(4, false) CH(8, false) CH(4, true) CH(8, true)
+    const int64_t nd = (int64_t)(bytes / 4), n2 = (int64_t)(bytes / 8);
+#define EL(T, NN, U, NAME) rep(NAME, timeit([&] { \
+        hipLaunchKernelGGL((copy_el<T, U>), dim3((unsigned)((NN + 256 * U - 1) / (256 * U))), dim3(256), 0, 0, (const T*)x, (T*)y, NN); }, 10));
+    EL(uint32_t, nd, 1, "one-shot dword, 1 per thread") EL(uint32_t, nd, 4, "one-shot dword, 4 per thread")
+    EL(uint32_t, nd, 16, "one-shot dword, 16 per thread") EL(uint2, n2, 1, "one-shot dwordx2, 1 per thread")
+    EL(uint2, n2, 4, "one-shot dwordx2, 4 per thread")
     return 0;
 }
