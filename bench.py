@@ -77,6 +77,10 @@ def parse():
                     help="skip the reference entry points' own (non-identity) lattices")
     ap.add_argument("--lattice-batch", type=int, default=32, help="4K images per lattice line")
     ap.add_argument("--pyramid-batch", type=int, default=8, help="8K images per GPU (config 5)")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="N > 1 with every rank on cuda:0 and the collectives over gloo (host "
+                         "staged): exercises the multi-rank bench path on a one-GPU box; the "
+                         "ranks share one GPU, so the value is not a scaling measurement")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-kernel HBM bytes from rocprofv3 PMC passes (optional)")
     return ap.parse_args()
@@ -226,11 +230,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    rehearse = world > 1 and args.rehearse_gloo
+    if rehearse:
+        local_rank = 0
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
+    cdev = torch.device("cpu") if rehearse else dev   # where the collectives' tensors live
 
     from HyGrid import ops
     from HyGrid.HexFrames import HexConv2d
@@ -278,11 +287,11 @@ def main():
         N > 1: the collective every timed step ends with (a few KB per rank).  One strided
         reduction kernel accumulating in fp32; nothing at N = 1 (no collective to feed)."""
         if world > 1:
-            s_ = torch.sum(y[:, :, ::64], (2, 3), dtype=torch.float32)
+            s_ = torch.sum(y[:, :, ::64], (2, 3), dtype=torch.float32).to(cdev)
             key = tuple(s_.shape)
             if key not in sums_buf:
                 sums_buf[key] = torch.empty((world * s_.shape[0],) + key[1:], dtype=s_.dtype,
-                                            device=s_.device)
+                                            device=cdev)
             gather_sums(s_, out=sums_buf[key])
 
     def measure(fn, steps, warmup, collective=True):
@@ -306,7 +315,7 @@ def main():
             if world > 1:
                 dist.barrier()
             t1 = time.perf_counter()
-        el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        el = torch.tensor([t1 - t0], dtype=torch.float64, device=cdev)
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         n = len(ev[0]) - 1
@@ -598,8 +607,8 @@ def main():
     cs = image_checksums(y)
     gather = None
     if world > 1:
-        cs = gather_checksums(cs)
-        if not args.no_gather:
+        cs = gather_checksums(cs.to(cdev))
+        if not args.no_gather and not rehearse:
             try:
                 gather_to_root(y)            # warm the RCCL channels
                 torch.cuda.synchronize()
@@ -637,7 +646,8 @@ def main():
             "config": {"workload": "config3: 4K RGB batch=128/GPU, rect->hex bilinear -> "
                                    "HexConv2d(3,3,off=0,r=2,pad=1) -> hex->rect linear",
                        "batch_per_gpu": B, "global_batch": B * world, "channels": C,
-                       "height": H, "width": W, "parallelism": f"dp{world}",
+                       "height": H, "width": W,
+                       "parallelism": f"dp{world}" + ("-rehearsal-gloo-1gpu" if rehearse else ""),
                        "fused": not args.unfused},
             "kernels": kernels, "roofline": roofline, "cpu_baseline": cpu,
             "unfused": compare, "roundtrip": roundtrip, "pyramid": pyramid, "wide_conv": wide,
