@@ -35,21 +35,27 @@ constexpr int FU_OWN = FU_OWN_;       // owned columns per 128-column window
 #ifndef FU_RB_PYR_
 #define FU_RB_PYR_ 60                 // MD 3 / 4: input rows per band (30 output rows)
 #endif
+#ifndef FU_RB_PYRS_
+#define FU_RB_PYRS_ 24                // MD 5 (= MD 4 on short bands for small levels)
+#endif
 #ifndef FU_RB_RT_
 #define FU_RB_RT_ 30                  // MD 2: rows per band (66 -> 30: 0.321 -> 0.307 ms, r03 A/B)
 #endif
 constexpr int FU_RB = FU_RB_;
 constexpr int FU_RB_CONV = FU_RB_CONV_;
 constexpr int FU_RB_PYR = FU_RB_PYR_;
+constexpr int FU_RB_PYRS = FU_RB_PYRS_;
 constexpr int FU_RB_RT = FU_RB_RT_;
 constexpr int fu_max(int a, int b) { return a > b ? a : b; }
-constexpr int FU_LUT = fu_max(fu_max(FU_RB, FU_RB_CONV), fu_max(FU_RB_PYR, FU_RB_RT)) + 2;
+constexpr int FU_LUT =
+    fu_max(fu_max(FU_RB, FU_RB_CONV), fu_max(fu_max(FU_RB_PYR, FU_RB_PYRS), FU_RB_RT)) + 2;
 // the one definition of a mode's band length, used by the kernel and the host launchers
 __host__ __device__ constexpr int fu_rb(int md) {
-    return md == 1 ? FU_RB_CONV : (md >= 3 ? FU_RB_PYR : (md == 2 ? FU_RB_RT : FU_RB));
+    return md == 1 ? FU_RB_CONV : md == 5 ? FU_RB_PYRS : md >= 3 ? FU_RB_PYR : md == 2 ? FU_RB_RT : FU_RB;
 }
-static_assert(FU_RB % 6 == 0 && FU_RB_CONV % 6 == 0 && FU_RB_PYR % 6 == 0 && FU_RB_RT % 6 == 0 &&
-              FU_RB > 0 && FU_RB_CONV > 0 && FU_RB_PYR > 0 && FU_RB_RT > 0,
+static_assert(FU_RB % 6 == 0 && FU_RB_CONV % 6 == 0 && FU_RB_PYR % 6 == 0 && FU_RB_PYRS % 6 == 0 &&
+              FU_RB_RT % 6 == 0 && FU_RB > 0 && FU_RB_CONV > 0 && FU_RB_PYR > 0 && FU_RB_PYRS > 0 &&
+              FU_RB_RT > 0,
               "bands are whole 6-step blocks (ring slots x row parities), even-aligned");
 static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
               "owned columns are whole lanes with a halo of >= 1 lane on each side");
@@ -302,7 +308,7 @@ __device__ __forceinline__ void fu_sfor(F&& f) {
 // MD 3 / 4: one hex-pyramid level (BASELINE config 5), the depthwise HexConv2d followed by
 // hexresize to (h / 2, w / 2) (geometry_np.py:520-681) for a 2x downsample: MD 3 from the
 // rect image (u rows made by r2h, as MD 0), MD 4 from a hex image (u rows = input rows, as
-// MD 1).  Every second step completes the two conv rows an output row's triangles read; a
+// MD 1; MD 5 = MD 4 on shorter bands, for levels too small to fill the chip).  Every second step completes the two conv rows an output row's triangles read; a
 // window of 128 input columns owns 60 output columns (lane l <-> output column W0/2 + l).
 template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD = 0>
 // MD 1 with 16-bit input and output fits 128 VGPRs (4 waves per SIMD); an fp32 raw ring or
@@ -316,7 +322,7 @@ void k_fused(const Tin* __restrict__ x,
     constexpr int CG = C / G, OG = O / G;
     constexpr int PD = FU_PD;
     constexpr bool PYR = MD >= 3;                 // hex-pyramid level (hexresize output stage)
-    constexpr bool UIN = MD == 1 || MD == 4;      // u rows = input rows (no r2h)
+    constexpr bool UIN = MD == 1 || MD >= 4;      // u rows = input rows (no r2h)
     constexpr bool VPK = FU_VPK && FU_PK && MD != 2 && !UIN;
     static_assert(PD >= 1 && PD <= 5, "raw ring: rows a2+2 .. a2+1+PD in flight in 6 slots");
     using Raw = typename RawOf<Tin>::type;

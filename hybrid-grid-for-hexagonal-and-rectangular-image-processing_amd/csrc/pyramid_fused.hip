@@ -34,11 +34,16 @@ static int pf_launch(const void* x, const float* taps, const float* bias, void* 
 
 template <typename Tin, typename Tout>
 static int pf_channels(const void* x, const float* taps, const float* bias, void* y,
-                       const FusedGeom& F, int C, int fr, int op, hipStream_t st) {
-    if (C == 3) return fr ? pf_launch<Tin, Tout, 3, 3>(x, taps, bias, y, F, op, st)
-                          : pf_launch<Tin, Tout, 3, 4>(x, taps, bias, y, F, op, st);
-    if (C == 1) return fr ? pf_launch<Tin, Tout, 1, 3>(x, taps, bias, y, F, op, st)
-                          : pf_launch<Tin, Tout, 1, 4>(x, taps, bias, y, F, op, st);
+                       const FusedGeom& F, int C, int md, int op, hipStream_t st) {
+#define HG_PF_MD(CC)                                                                          \
+    switch (md) {                                                                             \
+    case 3: return pf_launch<Tin, Tout, CC, 3>(x, taps, bias, y, F, op, st);                  \
+    case 4: return pf_launch<Tin, Tout, CC, 4>(x, taps, bias, y, F, op, st);                  \
+    default: return pf_launch<Tin, Tout, CC, 5>(x, taps, bias, y, F, op, st);                 \
+    }
+    if (C == 3) { HG_PF_MD(3) }
+    if (C == 1) { HG_PF_MD(1) }
+#undef HG_PF_MD
     return HG_EUNSUP;
 }
 
@@ -116,14 +121,23 @@ int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int6
         F.rys = r.ys;
     }
     F.nwin = (int)((w1 + FU_OWN / 2 - 1) / (FU_OWN / 2));
-    F.nband = (int)((h + fu_rb(3) - 1) / fu_rb(3));
+    // From a hex image: a level whose 60-row bands give fewer than six rounds of waves over
+    // the chip (256 CUs x 4 SIMDs x 4 waves) runs on short bands (MD 5): the last round of a
+    // launch that is only a few rounds long is mostly idle.  A/B switch HYGRID_PYR_SHORT=0/1.
+    int md = from_rect ? 3 : 4;
+    if (!from_rect) {
+        const int64_t waves = batch * ((h + fu_rb(4) - 1) / fu_rb(4)) * (int64_t)F.nwin;
+        bool shrt = waves < 6 * 4096;
+        if (const char* e = getenv("HYGRID_PYR_SHORT")) shrt = e[0] == '1';
+        if (shrt) md = 5;
+    }
+    F.nband = (int)((h + fu_rb(md) - 1) / fu_rb(md));
     const int op = (even_odd_offset + 1) & 1;   // tap column class at padding 1
-    const int fr = from_rect ? 1 : 0;
     if (src_dtype == HG_F16)
-        return dst_dtype == HG_F32 ? pf_channels<_Float16, float>(src, taps, bias, dst, F, (int)C, fr, op, st)
-                                   : pf_channels<_Float16, _Float16>(src, taps, bias, dst, F, (int)C, fr, op, st);
-    return dst_dtype == HG_F32 ? pf_channels<__bf16, float>(src, taps, bias, dst, F, (int)C, fr, op, st)
-                               : pf_channels<__bf16, __bf16>(src, taps, bias, dst, F, (int)C, fr, op, st);
+        return dst_dtype == HG_F32 ? pf_channels<_Float16, float>(src, taps, bias, dst, F, (int)C, md, op, st)
+                                   : pf_channels<_Float16, _Float16>(src, taps, bias, dst, F, (int)C, md, op, st);
+    return dst_dtype == HG_F32 ? pf_channels<__bf16, float>(src, taps, bias, dst, F, (int)C, md, op, st)
+                               : pf_channels<__bf16, __bf16>(src, taps, bias, dst, F, (int)C, md, op, st);
 }
 
 }  // namespace hg

@@ -281,3 +281,35 @@ def test_pyramid_level_stream_vs_oracle_and_lds(case, off, dt, from_rect, monkey
     got = y.double().cpu().numpy()
     np.testing.assert_allclose(got, ref, rtol=ulp, atol=ulp * scale)
     torch.testing.assert_close(y.float(), y_lds.float(), rtol=2 * ulp, atol=2 * ulp * scale)
+
+
+@pytest.mark.parametrize("case", STREAM_CASES + [(8, 3, 1080, 1920)])
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_pyramid_level_short_bands_vs_oracle(case, dt, monkeypatch):
+    """A level from a hex image on the fused row walk with 60-row bands (MD 4) and with the
+    short bands small levels take (MD 5, HYGRID_PYR_SHORT=1): bit-identical to each other
+    (a band split changes no output's arithmetic) and within one output rounding of the fp64
+    oracle chain.  (8, 3, 1080, 1920) is the bench's level 2 at full size."""
+    B, C, h, w = case
+    h1, w1 = h // 2, w // 2
+    g = torch.Generator().manual_seed(h + 7 * w)
+    taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
+    bias = (torch.rand((C,), generator=g) - 0.5).to(DEV)
+    x = torch.rand((B, C, h, w), generator=g).to(DEV).to(dt)
+    monkeypatch.setenv("HYGRID_PYRSTREAM", "only")
+    outs = []
+    for short in ("0", "1"):
+        monkeypatch.setenv("HYGRID_PYR_SHORT", short)
+        outs.append(ops.hex_pyramid_level(x, taps, bias, (h1, w1), 1))
+    monkeypatch.delenv("HYGRID_PYR_SHORT")
+    monkeypatch.delenv("HYGRID_PYRSTREAM")
+    assert outs[0] is not None and outs[1] is not None
+    assert torch.equal(outs[0], outs[1])
+    n = 1 if B * h * w > 1 << 22 else B          # full-size case: the first image
+    xd = x[:n].double().cpu().numpy()
+    c = O.hexconv2d(xd, taps.cpu().double().numpy(), bias.cpu().double().numpy(), 1, 2,
+                    padding=1, groups=C)
+    ref = O.hexresize(c, (h1, w1), 1).reshape(n, C, h1, w1)
+    ulp = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
+    scale = float(np.abs(ref).max())
+    np.testing.assert_allclose(outs[1][:n].double().cpu().numpy(), ref, rtol=ulp, atol=ulp * scale)

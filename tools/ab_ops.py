@@ -4,9 +4,9 @@ variant three times back to back in a shuffled order and times the last launch; 
 min per launch and the median per-round ratio to the first variant named).
 
 usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
-  OP: r2h | h2r | conv | wide (HexConv2d 64->64, 1080p bf16 b4) | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1   (bf16 4K b128 for
+  OP: r2h | h2r | conv | wide (HexConv2d 64->64, 1080p bf16 b4) | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1 | pyr2   (bf16 4K b128 for
       r2h/h2r/conv; fp32 1080p b32 for r2h32/h2r32 and rt, the fused round trip; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K from a
-      hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K)
+      hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K, pyr2 = level 2, 2K -> 1K)
   name 'base' = the in-tree library; others = HyGrid/_lib/variants/libhygrid_<name>.so;
   'name%VAR=VAL' runs that library with the environment variable VAR=VAL set around its calls
   (the library's A/B switches, e.g. base%HYGRID_PYRSTREAM=0)
@@ -49,6 +49,8 @@ def main():
         B, C, H, W, t = 4, 64, 1080, 1920, torch.bfloat16
     elif op == "pyr1":
         B, C, H, W, t = 8, 3, 2160, 3840, torch.float16
+    elif op == "pyr2":
+        B, C, H, W, t = 8, 3, 1080, 1920, torch.float16
     else:
         B, C, H, W, t = 8, 3, 4320, 7680, torch.float16
     x = torch.rand((B, C, H, W), generator=g, device=dev, dtype=t)
