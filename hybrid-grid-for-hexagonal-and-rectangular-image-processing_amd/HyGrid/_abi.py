@@ -26,6 +26,8 @@ HG_U8, HG_I8, HG_U16, HG_I16, HG_I32, HG_I64, HG_F16, HG_BF16, HG_F32, HG_F64 = 
 HG_NEAREST, HG_LINEAR = 0, 1
 HG_OP_RECT_TO_HEX, HG_OP_HEX_TO_RECT, HG_OP_HEXRESIZE = 0, 1, 2
 HG_KERNEL_GENERAL, HG_KERNEL_NEAREST, HG_KERNEL_STREAM, HG_KERNEL_DOWN = range(4)
+HG_PYR_FUSED, HG_PYR_FUSED_SHORT, HG_PYR_STREAM, HG_PYR_LDS = range(4)
+HG_OK, HG_EINVAL, HG_EDTYPE, HG_ESHAPE, HG_EUNSUP, HG_EOVERFLOW = 0, -1, -2, -3, -4, -5
 PAD_MODES = {"constant": 0, "zeros": 0, "reflect": 1, "replicate": 2, "circular": 3}
 HG_ACT_NONE, HG_ACT_RELU, HG_ACT_LEAKY_RELU, HG_ACT_RELU6, HG_ACT_SIGMOID, HG_ACT_TANH = range(6)
 
@@ -72,6 +74,7 @@ SIGNATURES = {
                                + [_i64, _i64, _vp], _int),
     "hg_hex_pyramid_level": ([_vp, _vp, _int, _int] + [_i64] * 6 + [_vp, _vp, _int, _int, _vp],
                              _int),
+    "hg_hex_pyramid_level_kernel": ([_int, _int] + [_i64] * 6 + [_int, _int], _int),
     "hg_pipeline_r2h_h2r": ([_vp, _vp, _int, _int] + [_i64] * 5 + [_vp], _int),
     "hg_pipeline_r2h_conv_h2r": ([_vp, _vp, _vp, _vp, _int, _int] + [_i64] * 9 +
                                  [_int, _int, _int, _dbl, _vp], _int),
@@ -126,6 +129,17 @@ def resample_kernel(op, src_dtype, dst_dtype, planes, h, w, h1, w1, interp=HG_LI
                                   int(w), int(h1), int(w1), int(interp))
     if st < 0:
         check(st, "hg_resample_kernel")
+    return st
+
+
+def pyramid_level_kernel(x_dtype, y_dtype, batch, channels, h, w, h1, w1, even_odd_offset=0,
+                         from_rect=False):
+    """Which kernel hg_hex_pyramid_level would run (HG_PYR_*; nothing is launched)."""
+    st = lib().hg_hex_pyramid_level_kernel(int(x_dtype), int(y_dtype), int(batch), int(channels),
+                                           int(h), int(w), int(h1), int(w1), int(even_odd_offset),
+                                           int(bool(from_rect)))
+    if st < 0:
+        check(st, "hg_hex_pyramid_level_kernel")
     return st
 
 

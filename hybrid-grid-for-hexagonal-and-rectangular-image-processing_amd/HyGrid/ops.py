@@ -436,7 +436,7 @@ def strided_copy2d(x, row_start, row_step, col_start, col_step, h_out=None, w_ou
     return y
 
 
-HG_EUNSUP = -4
+HG_EUNSUP = _abi.HG_EUNSUP
 
 
 def pipeline_r2h_h2r(x, hex_size=None, out_dtype=None):
@@ -458,7 +458,7 @@ def pipeline_r2h_h2r(x, hex_size=None, out_dtype=None):
     st = _abi.lib().hg_pipeline_r2h_h2r(_abi.ptr(x), _abi.ptr(y), _abi.dtype_code(x.dtype),
                                         _abi.dtype_code(out_dtype), planes, h, w, h1, w1,
                                         _abi.stream_of(x))
-    if st in (HG_EUNSUP, -2):
+    if st in (HG_EUNSUP, _abi.HG_EDTYPE):
         return None
     _abi.check(st, "hg_pipeline_r2h_h2r")
     return y
@@ -489,7 +489,7 @@ def pipeline_r2h_conv_h2r(x, kernel, bias, hex_size=None, rect_size=None, paddin
         _abi.ptr(x), _abi.ptr(k), _abi.ptr(b), _abi.ptr(y), _abi.dtype_code(x.dtype),
         _abi.dtype_code(out_dtype), B, C, O, h, w, h1, w1, h2, w2, int(padding), int(groups),
         int(even_odd_offset), float(padding_value), _abi.stream_of(x))
-    if st in (HG_EUNSUP, -2):
+    if st in (HG_EUNSUP, _abi.HG_EDTYPE):
         return None
     _abi.check(st, "hg_pipeline_r2h_conv_h2r")
     return y
@@ -520,7 +520,7 @@ def hex_pyramid_level(x, taps, bias=None, size=None, even_odd_offset=0, from_rec
         _abi.ptr(x), _abi.ptr(y), _abi.dtype_code(x.dtype), _abi.dtype_code(out_dtype), B, C,
         h, w, h1, w1, _abi.ptr(k), _abi.ptr(b), int(even_odd_offset), int(bool(from_rect)),
         _abi.stream_of(x))
-    if st in (HG_EUNSUP, -2):
+    if st in (HG_EUNSUP, _abi.HG_EDTYPE):
         return None
     _abi.check(st, "hg_hex_pyramid_level")
     return y

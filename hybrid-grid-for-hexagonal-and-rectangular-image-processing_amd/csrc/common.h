@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "../../include/hygrid.h"
 
@@ -48,6 +50,13 @@ inline bool acc_is_double(int in_dt, int out_dt) {
 inline int hip_status(hipError_t e) { return e == hipSuccess ? HG_OK : (int)e; }
 
 inline int launch_status() { return hip_status(hipGetLastError()); }
+
+// The library's A/B / test switches (HYGRID_*, read on every call): true iff the variable is
+// set to exactly `value`.
+inline bool env_is(const char* name, const char* value) {
+    const char* e = getenv(name);
+    return e && !strcmp(e, value);
+}
 
 // XCD-aware block order.  Blocks are dealt to the 8 XCDs round-robin (bid % 8 labels
 // the blocks that share an XCD and its private L2); this bijection hands each XCD a

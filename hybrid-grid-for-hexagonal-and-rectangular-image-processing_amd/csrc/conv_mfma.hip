@@ -329,9 +329,7 @@ int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_
                   int y_dtype, int64_t B, int64_t C, int64_t O, int64_t h, int64_t w, int radius,
                   int stride, int padding, int dilation, int groups, int off, int pad_mode,
                   double pad_value, const Epilogue& epi, hipStream_t st) {
-    if (const char* e = getenv("HYGRID_CONV_MFMA")) {   // A/B switch: 0 = generic kernels
-        if (e[0] == '0') return HG_EUNSUP;
-    }
+    if (env_is("HYGRID_CONV_MFMA", "0")) return HG_EUNSUP;   // A/B switch: generic kernels
     if (radius != 2 || stride != 1 || dilation != 1 || groups != 1) return HG_EUNSUP;
     if (C < 8 || O < 16 || padding < 0 || padding > 2) return HG_EUNSUP;
     if (C > INT_MAX / 16 || O > INT_MAX / 16 || h > INT_MAX / 4 || w > INT_MAX / 4) return HG_EUNSUP;
@@ -367,8 +365,8 @@ int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_
     // bf16 inputs: the split-weight bf16 kernel, when the pad value is a bf16 (the padded
     // input keeps the input's dtype, as F.pad does; anything else keeps the f32 kernel)
     const bool bf_pad = (double)(float)(__bf16)(float)pad_value == pad_value;
-    const char* eb = getenv("HYGRID_CONV_MFMA_BF16");   // A/B switch: 0 = the f32 kernel
-    if (x_dtype == HG_BF16 && bf_pad && !(eb && eb[0] == '0') &&
+    // A/B switch HYGRID_CONV_MFMA_BF16=0: the f32 kernel
+    if (x_dtype == HG_BF16 && bf_pad && !env_is("HYGRID_CONV_MFMA_BF16", "0") &&
         (y_dtype == HG_BF16 || y_dtype == HG_F32)) {
 #define HG_CB_LAUNCH(TO)                                                                      \
         if (nt == 2)                                                                          \

@@ -87,9 +87,7 @@ static bool fused_geometry_ok(const Geom& g) {
 // image kept on chip in fp32.
 int fused_rt_try(const void* x, void* y, int x_dtype, int y_dtype, int64_t planes, int64_t h,
                  int64_t w, int64_t h1, int64_t w1, hipStream_t st) {
-    if (const char* e = getenv("HYGRID_FUSED2")) {   // A/B switch for measurements
-        if (e[0] == '0') return HG_EUNSUP;
-    }
+    if (env_is("HYGRID_FUSED2", "0")) return HG_EUNSUP;   // A/B switch for measurements
     if ((w & 1) || (w1 & 1) || w < 2 || h1 < 1 || planes < 1) return HG_EUNSUP;
     if (x_dtype != HG_BF16 && x_dtype != HG_F16 && x_dtype != HG_F32) return HG_EUNSUP;
     if (y_dtype != HG_BF16 && y_dtype != HG_F16 && y_dtype != HG_F32) return HG_EUNSUP;
@@ -123,9 +121,7 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
               int y_dtype, int64_t batch, int C, int O, int G, int64_t h, int64_t w,
               int64_t h1, int64_t w1, int64_t h2, int64_t w2, int padding, int op,
               double pad_value, hipStream_t st) {
-    if (const char* e = getenv("HYGRID_FUSED2")) {   // A/B switch for measurements
-        if (e[0] == '0') return HG_EUNSUP;
-    }
+    if (env_is("HYGRID_FUSED2", "0")) return HG_EUNSUP;   // A/B switch for measurements
     if (padding != 1 || pad_value != 0.0) return HG_EUNSUP;
     if (h2 != h1 || w2 != w1) return HG_EUNSUP;       // ho = h1, wo = w1 at padding 1
     if ((w & 1) || (w1 & 1) || w < 2 || h1 < 1) return HG_EUNSUP;   // dword column pairs

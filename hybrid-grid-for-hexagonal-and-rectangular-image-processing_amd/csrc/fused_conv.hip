@@ -38,9 +38,7 @@ static int fconv_channels(const void* x, const float* k, const float* b, void* y
 int fused_conv_try(const void* x, const float* kernel, const float* bias, void* y, int x_dtype,
                    int y_dtype, int64_t batch, int C, int O, int G, int64_t h, int64_t w,
                    int padding, int off, double pad_value, bool epilogue, hipStream_t st) {
-    if (const char* e = getenv("HYGRID_FCONV")) {    // A/B switch: 0 = conv_stream kernel
-        if (e[0] == '0') return HG_EUNSUP;
-    }
+    if (env_is("HYGRID_FCONV", "0")) return HG_EUNSUP;   // A/B switch: conv_stream kernel
     if (epilogue || padding != 1 || pad_value != 0.0) return HG_EUNSUP;
     if ((w & 1) || w < 2 || h < 1 || batch < 1) return HG_EUNSUP;   // dword column pairs
     if (C * h * w * 8 >= ((int64_t)1 << 31) || O * h * w * 4 >= ((int64_t)1 << 31))

@@ -26,6 +26,8 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
+#include <vector>
 
 #include "common.h"
 #include "lattice.h"
@@ -35,11 +37,13 @@ namespace hg {
 // pyramid_stream.hip: the register-streaming level for 2x downsamples (HG_EUNSUP otherwise)
 int pyr_stream_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
                    int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
-                   const float* bias, int even_odd_offset, int from_rect, hipStream_t st);
+                   const float* bias, int even_odd_offset, int from_rect, hipStream_t st,
+                   bool dry);
 // pyramid_fused.hip: the same level on the streaming fused kernel (tried first)
 int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
                   int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
-                  const float* bias, int even_odd_offset, int from_rect, hipStream_t st);
+                  const float* bias, int even_odd_offset, int from_rect, hipStream_t st,
+                  bool dry);
 
 constexpr int PY_THREADS = 256;
 constexpr int PY_TZR = 16;                 // output tile rows
@@ -70,6 +74,8 @@ struct PyrGeom {
     const float* bias;         // [C] or null
     Geom tri;                  // hexresize lattice (h, w) -> (h1, w1)
     Geom r2h;                  // rect_to_hex lattice (h, w) -> (h, w) (from_rect)
+    int cap_yr, cap_yc;        // Y footprint capacity (PY_YR, PY_YC; smaller only in tests)
+    int* fault;                // set to 1 by a workgroup whose footprint overflows its tile
 };
 
 // r=2, padding-1 tap geometry (fused_kernel.h): tap t of an output row of parity `par`
@@ -197,10 +203,12 @@ __global__ __launch_bounds__(PY_THREADS) void k_pyr_level(const Tin* __restrict_
     // a tile whose samples all fall outside the raster still stores its zeros
     const int ry0 = any_valid ? red[0] : 0, cy0 = any_valid ? red[2] : 0;
     const int yr = any_valid ? red[1] - red[0] + 1 : 1, yc = any_valid ? red[3] - red[2] + 1 : 1;
-    // Footprint larger than the LDS tile: the host check (pyr_footprint_ok) samples rows and
-    // adds a skew margin, so this is not expected; if it happens, the tile's outputs are
-    // written as NaN rather than left uninitialised, so the failure is visible.
+    // Footprint larger than the LDS tile: the host bound (pyr_footprint_ok) is exact, so
+    // this cannot happen for a launch it admitted; if it does (a test drives it with a
+    // smaller cap), the workgroup raises the call's fault flag -- hg_hex_pyramid_level then
+    // returns HG_EOVERFLOW -- and writes its outputs as NaN instead of leaving them unset.
     auto poison = [&]() {
+        if (tid == 0) atomicOr(G.fault, 1);
         for (int64_t p = p0; p < p1; ++p)
             for (int k = tid; k < PY_TZR * PY_TZC; k += PY_THREADS) {
                 const int a = a0 + k / PY_TZC, b = b0 + k % PY_TZC;
@@ -208,7 +216,7 @@ __global__ __launch_bounds__(PY_THREADS) void k_pyr_level(const Tin* __restrict_
                     dst[(p * G.h1 + a) * (int64_t)G.w1 + b] = (Tout)__builtin_nanf("");
             }
     };
-    if (yr > PY_YR || yc > PY_YC) { poison(); return; }
+    if (yr > G.cap_yr || yc > G.cap_yc) { poison(); return; }
     int zo[PY_NZ][3];
 #pragma unroll
     for (int i = 0; i < PY_NZ; ++i)
@@ -421,29 +429,38 @@ static bool r2h_near_identity(const Geom& g) {
     return true;
 }
 
-// Exact Y footprint of every output tile fits the LDS tile?  The triangle taps of a
-// sample are rows i_n, i_n+1 and columns within [c1-1, c1+1]; evaluating the lattice at
-// the tile's corner rows/columns bounds it (i_n and c are monotone along each axis).
-static bool pyr_footprint_ok(const Geom& g) {
+// Does the Y footprint of every output tile fit cap_r x cap_c?  A sample's triangle
+// vertices lie in rows i_n, i_n + 1 and columns j_n - s2 .. j_n + 1 - s1 (s1 = (i_n + 1) / 2,
+// s2 = (i_n + 2) / 2; geometry_np.py:289-322, lattice.h tri_sample_xy).  i_n depends on the row
+// a only and grows with it; j_n grows with the column b for a fixed row.  So per tile column
+// [b0, b1] and row a the columns span [j_n(a, b0) - s2(a), j_n(a, b1) + 1 - s1(a)], and a
+// tile's footprint is the union over its rows: an exact bound on the kernel's reduction
+// (which counts only the vertices inside the raster), O(h1) per tile column.
+static bool pyr_footprint_ok(const Geom& g, int cap_r, int cap_c) {
     const int64_t nty = (g.h1 + PY_TZR - 1) / PY_TZR, ntx = (g.w1 + PY_TZC - 1) / PY_TZC;
     for (int64_t ty = 0; ty < nty; ++ty) {
         const int64_t a0 = ty * PY_TZR, a1 = std::min<int64_t>(a0 + PY_TZR, g.h1) - 1;
         const TriSample s0 = tri_sample(g, a0, 0), s1 = tri_sample(g, a1, 0);
-        if (s1.r[2] - s0.r[0] + 1 > PY_YR) return false;
+        if (s1.i_n + 1 - s0.i_n + 1 > cap_r) return false;
     }
+    std::vector<int64_t> lo(g.h1), hi(g.h1);
     for (int64_t tx = 0; tx < ntx; ++tx) {
         const int64_t b0 = tx * PY_TZC, b1 = std::min<int64_t>(b0 + PY_TZC, g.w1) - 1;
-        int64_t lo = INT64_MAX, hi = INT64_MIN;
-        for (int64_t a : {(int64_t)0, (int64_t)1, g.h1 / 2, g.h1 / 2 + 1, g.h1 - 2, g.h1 - 1}) {
-            if (a < 0 || a >= g.h1) continue;
+        for (int64_t a = 0; a < g.h1; ++a) {
             const TriSample s0 = tri_sample(g, a, b0), s1 = tri_sample(g, a, b1);
-            for (int m = 0; m < 3; ++m) {
-                lo = std::min(lo, std::min(s0.c[m], s1.c[m]));
-                hi = std::max(hi, std::max(s0.c[m], s1.c[m]));
-            }
+            const int64_t q1 = (int64_t)((double)(s0.i_n + 1) / 2.0), q2 = (int64_t)((double)(s0.i_n + 2) / 2.0);
+            lo[a] = s0.j_n - q2;
+            hi[a] = s1.j_n + 1 - q1;
         }
-        if (hi - lo + 1 + 2 > PY_YC) return false;   // +2: column skew between rows
-        // (the X tile adds 1 + 2 columns and 1 for its even origin: PY_XP = PY_YC + 6)
+        for (int64_t ty = 0; ty < nty; ++ty) {
+            const int64_t a0 = ty * PY_TZR, a1 = std::min<int64_t>(a0 + PY_TZR, g.h1);
+            int64_t l = INT64_MAX, u = INT64_MIN;
+            for (int64_t a = a0; a < a1; ++a) {
+                l = std::min(l, lo[a]);
+                u = std::max(u, hi[a]);
+            }
+            if (u - l + 1 > cap_c) return false;
+        }
     }
     return true;
 }
@@ -455,9 +472,23 @@ static int pyr_launch(const void* src, void* dst, PyrGeom& G, hipStream_t st) {
     nchunk = std::min<int64_t>(nchunk, 65535);
     G.pc = (int)((G.planes + nchunk - 1) / nchunk);
     const dim3 grid((unsigned)tiles, (unsigned)((G.planes + G.pc - 1) / G.pc));
-    hipLaunchKernelGGL((k_pyr_level<FR, OP, Tin, Tout>), grid, dim3(PY_THREADS), 0, st,
-                       (const Tin*)src, (Tout*)dst, G);
-    return launch_status();
+    // the fault flag: one word per call (reentrant), read back after the launch
+    int* fault = nullptr;
+    hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&fault), sizeof(int), st);
+    if (e != hipSuccess) return (int)e;
+    G.fault = fault;
+    int rc = (int)hipMemsetAsync(fault, 0, sizeof(int), st);
+    if (rc == HG_OK) {
+        hipLaunchKernelGGL((k_pyr_level<FR, OP, Tin, Tout>), grid, dim3(PY_THREADS), 0, st,
+                           (const Tin*)src, (Tout*)dst, G);
+        rc = launch_status();
+    }
+    int hf = 0;
+    if (rc == HG_OK) rc = (int)hipMemcpyAsync(&hf, fault, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (rc == HG_OK) rc = (int)hipStreamSynchronize(st);
+    (void)hipFreeAsync(fault, st);
+    if (rc == HG_OK && hf) rc = HG_EOVERFLOW;
+    return rc;
 }
 
 template <typename Tin, typename Tout>
@@ -468,19 +499,45 @@ static int pyr_dispatch(const void* src, void* dst, PyrGeom& G, int from_rect, i
     return op ? pyr_launch<0, 1, Tin, Tout>(src, dst, G, st) : pyr_launch<0, 0, Tin, Tout>(src, dst, G, st);
 }
 
-}  // namespace hg
+static bool pyr_dtypes_ok(int src_dtype, int dst_dtype) {
+    switch (src_dtype) {
+    case HG_F16: return dst_dtype == HG_F16 || dst_dtype == HG_F32;
+    case HG_BF16: return dst_dtype == HG_BF16 || dst_dtype == HG_F32;
+    case HG_F32: return dst_dtype == HG_F32 || dst_dtype == HG_F16 || dst_dtype == HG_BF16;
+    default: return false;
+    }
+}
 
-extern "C" int hg_hex_pyramid_level(const void* src, void* dst, int src_dtype, int dst_dtype,
-                                    int64_t batch, int64_t channels, int64_t h, int64_t w,
-                                    int64_t h1, int64_t w1, const float* taps,
-                                    const float* bias, int even_odd_offset, int from_rect,
-                                    void* stream) {
-    using namespace hg;
+// One level: the fused kernel, else k_pyr_stream, else k_pyr_level (each declines with
+// HG_EUNSUP outside its domain).  dry: return the kernel that would run, launch nothing.
+// HYGRID_PYR_KERNEL = "fused" | "stream" | "lds" restricts the choice to one kernel (tests,
+// A/B).  HYGRID_PYR_LDS_FORCE_CAP = <rows> (tests only): skip the host footprint bound and
+// give k_pyr_level a tile of that many rows, to drive its overflow branch.
+static int pyr_level(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
+                     int64_t channels, int64_t h, int64_t w, int64_t h1, int64_t w1,
+                     const float* taps, const float* bias, int even_odd_offset, int from_rect,
+                     hipStream_t st, bool dry) {
     if (batch < 0 || channels < 1 || h < 1 || w < 1 || h1 < 1 || w1 < 1) return HG_EINVAL;
-    if (!taps || (batch > 0 && (!src || !dst))) return HG_EINVAL;
+    if (!dry && (!taps || (batch > 0 && (!src || !dst)))) return HG_EINVAL;
     if (even_odd_offset != 0 && even_odd_offset != 1) return HG_EINVAL;
     if (h * w >= INT_MAX / 2 || h1 * w1 >= INT_MAX / 2) return HG_ESHAPE;
-    if (batch == 0) return HG_OK;
+    if (!pyr_dtypes_ok(src_dtype, dst_dtype)) return HG_EDTYPE;
+    if (batch == 0) return dry ? HG_PYR_LDS : HG_OK;
+    // a restriction to one kernel, or null (unset, "auto" or any other value: no restriction)
+    const char* force = nullptr;
+    for (const char* k : {"fused", "stream", "lds"})
+        if (env_is("HYGRID_PYR_KERNEL", k)) force = k;
+    if (!force || !strcmp(force, "fused")) {
+        const int rc = pyr_fused_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1, w1,
+                                     taps, bias, even_odd_offset, from_rect, st, dry);
+        if (rc != HG_EUNSUP) return rc;
+    }
+    if (!force || !strcmp(force, "stream")) {
+        const int rc = pyr_stream_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1,
+                                      w1, taps, bias, even_odd_offset, from_rect, st, dry);
+        if (rc != HG_EUNSUP) return rc;
+    }
+    if (force && strcmp(force, "lds")) return HG_EUNSUP;
     PyrGeom G = {};
     G.planes = batch * channels;
     G.C = (int)channels;
@@ -492,41 +549,48 @@ extern "C" int hg_hex_pyramid_level(const void* src, void* dst, int src_dtype, i
     G.bias = bias;
     G.tri = make_tri(h, w, h1, w1, 0.5);
     G.r2h = make_r2h(h, w, h, w);
+    G.cap_yr = PY_YR;
+    G.cap_yc = PY_YC;
     if ((int64_t)G.ntx * G.nty > INT_MAX) return HG_ESHAPE;
-    if (!pyr_footprint_ok(G.tri)) return HG_EUNSUP;
     // dword staging of 16-bit rasters: rows must start on a dword (even width, 4-B base)
     if (dtype_size(src_dtype) == 2 && ((w & 1) || (reinterpret_cast<uintptr_t>(src) & 3)))
         return HG_EUNSUP;
     if (from_rect && !r2h_near_identity(G.r2h)) return HG_EUNSUP;
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    {
-        int rc = pyr_fused_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1, w1,
-                               taps, bias, even_odd_offset, from_rect, st);
-        if (rc != HG_EUNSUP) return rc;
-        rc = pyr_stream_try(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1,
-                            w1, taps, bias, even_odd_offset, from_rect, st);
-        if (rc != HG_EUNSUP) return rc;
-        // test hook: HYGRID_PYRSTREAM=only declines instead of falling back to the LDS kernel,
-        // so a test can assert that a streaming kernel (fused or k_pyr_stream) is what ran
-        if (const char* e = getenv("HYGRID_PYRSTREAM")) {
-            if (e[0] == 'o') return HG_EUNSUP;
-        }
+    const char* cap = getenv("HYGRID_PYR_LDS_FORCE_CAP");   // tests only
+    if (cap && atoi(cap) > 0) {
+        G.cap_yr = std::min(PY_YR, atoi(cap));
+    } else if (!pyr_footprint_ok(G.tri, PY_YR, PY_YC)) {
+        return HG_EUNSUP;
     }
+    if (dry) return HG_PYR_LDS;
     switch (src_dtype) {
     case HG_F16:
         if (dst_dtype == HG_F16) return pyr_dispatch<_Float16, _Float16>(src, dst, G, from_rect, op, st);
-        if (dst_dtype == HG_F32) return pyr_dispatch<_Float16, float>(src, dst, G, from_rect, op, st);
-        return HG_EDTYPE;
+        return pyr_dispatch<_Float16, float>(src, dst, G, from_rect, op, st);
     case HG_BF16:
         if (dst_dtype == HG_BF16) return pyr_dispatch<__bf16, __bf16>(src, dst, G, from_rect, op, st);
-        if (dst_dtype == HG_F32) return pyr_dispatch<__bf16, float>(src, dst, G, from_rect, op, st);
-        return HG_EDTYPE;
-    case HG_F32:
+        return pyr_dispatch<__bf16, float>(src, dst, G, from_rect, op, st);
+    default:
         if (dst_dtype == HG_F32) return pyr_dispatch<float, float>(src, dst, G, from_rect, op, st);
         if (dst_dtype == HG_F16) return pyr_dispatch<float, _Float16>(src, dst, G, from_rect, op, st);
-        if (dst_dtype == HG_BF16) return pyr_dispatch<float, __bf16>(src, dst, G, from_rect, op, st);
-        return HG_EDTYPE;
-    default:
-        return HG_EDTYPE;
+        return pyr_dispatch<float, __bf16>(src, dst, G, from_rect, op, st);
     }
+}
+
+}  // namespace hg
+
+extern "C" int hg_hex_pyramid_level(const void* src, void* dst, int src_dtype, int dst_dtype,
+                                    int64_t batch, int64_t channels, int64_t h, int64_t w,
+                                    int64_t h1, int64_t w1, const float* taps,
+                                    const float* bias, int even_odd_offset, int from_rect,
+                                    void* stream) {
+    return hg::pyr_level(src, dst, src_dtype, dst_dtype, batch, channels, h, w, h1, w1, taps, bias,
+                         even_odd_offset, from_rect, reinterpret_cast<hipStream_t>(stream), false);
+}
+
+extern "C" int hg_hex_pyramid_level_kernel(int x_dtype, int y_dtype, int64_t batch,
+                                           int64_t channels, int64_t h, int64_t w, int64_t h1,
+                                           int64_t w1, int even_odd_offset, int from_rect) {
+    return hg::pyr_level(nullptr, nullptr, x_dtype, y_dtype, batch, channels, h, w, h1, w1, nullptr,
+                         nullptr, even_odd_offset, from_rect, nullptr, true);
 }

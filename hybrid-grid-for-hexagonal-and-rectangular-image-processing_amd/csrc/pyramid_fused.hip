@@ -8,10 +8,12 @@
 // FMAs into three conv-row accumulators — with the hexresize triangle as its output stage:
 // every second step completes the two conv rows one output row reads.  Tried first by
 // hg_hex_pyramid_level (pyramid.hip); returns HG_EUNSUP outside its domain (then
-// k_pyr_stream, then k_pyr_level).
+// k_pyr_stream, then k_pyr_level).  With `dry` nothing is launched and the kernel that
+// would run (HG_PYR_FUSED / HG_PYR_FUSED_SHORT) is returned.
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstring>
 
 #include "fused_kernel.h"
 
@@ -93,10 +95,8 @@ static bool pf_r2h_ok(const Geom& g) {
 
 int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
                   int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
-                  const float* bias, int even_odd_offset, int from_rect, hipStream_t st) {
-    if (const char* e = getenv("HYGRID_PYRFUSED")) {   // A/B switch: 0 = k_pyr_stream
-        if (e[0] == '0') return HG_EUNSUP;
-    }
+                  const float* bias, int even_odd_offset, int from_rect, hipStream_t st,
+                  bool dry) {
     if (C != 1 && C != 3) return HG_EUNSUP;
     if ((w & 1) || w < 2 || h < 2 || h1 < 1 || w1 < 1 || batch < 1) return HG_EUNSUP;
     if (src_dtype != HG_F16 && src_dtype != HG_BF16) return HG_EUNSUP;
@@ -123,14 +123,17 @@ int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int6
     F.nwin = (int)((w1 + FU_OWN / 2 - 1) / (FU_OWN / 2));
     // From a hex image: a level whose 60-row bands give fewer than six rounds of waves over
     // the chip (256 CUs x 4 SIMDs x 4 waves) runs on short bands (MD 5): the last round of a
-    // launch that is only a few rounds long is mostly idle.  A/B switch HYGRID_PYR_SHORT=0/1.
+    // launch that is only a few rounds long is mostly idle.  A/B switch HYGRID_PYR_SHORT=0/1
+    // (exactly "0" or "1"; anything else: the rule above).
     int md = from_rect ? 3 : 4;
     if (!from_rect) {
         const int64_t waves = batch * ((h + fu_rb(4) - 1) / fu_rb(4)) * (int64_t)F.nwin;
         bool shrt = waves < 6 * 4096;
-        if (const char* e = getenv("HYGRID_PYR_SHORT")) shrt = e[0] == '1';
+        if (env_is("HYGRID_PYR_SHORT", "1")) shrt = true;
+        if (env_is("HYGRID_PYR_SHORT", "0")) shrt = false;
         if (shrt) md = 5;
     }
+    if (dry) return md == 5 ? HG_PYR_FUSED_SHORT : HG_PYR_FUSED;
     F.nband = (int)((h + fu_rb(md) - 1) / fu_rb(md));
     const int op = (even_odd_offset + 1) & 1;   // tap column class at padding 1
     if (src_dtype == HG_F16)

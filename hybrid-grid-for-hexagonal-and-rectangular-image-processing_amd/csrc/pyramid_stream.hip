@@ -441,12 +441,11 @@ static bool ps_r2h_near_identity(const Geom& g) {
 
 // One pyramid level on the streaming kernel, or HG_EUNSUP (the caller runs k_pyr_level).
 // from_rect: src is the rect image and the level input is its same-size rect_to_hex.
+// dry: launch nothing, return HG_PYR_STREAM if the kernel would run.
 int pyr_stream_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
                    int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
-                   const float* bias, int even_odd_offset, int from_rect, hipStream_t st) {
-    if (const char* e = getenv("HYGRID_PYRSTREAM")) {   // A/B switch for measurements
-        if (e[0] == '0') return HG_EUNSUP;
-    }
+                   const float* bias, int even_odd_offset, int from_rect, hipStream_t st,
+                   bool dry) {
     if (C != 1 && C != 3) return HG_EUNSUP;
     if ((w & 1) || w < 2 || h < 2 || h1 < 1 || w1 < 1) return HG_EUNSUP;
     if (src_dtype != dst_dtype || (src_dtype != HG_F16 && src_dtype != HG_BF16)) return HG_EUNSUP;
@@ -471,6 +470,7 @@ int pyr_stream_try(const void* src, void* dst, int src_dtype, int dst_dtype, int
         G.rxs = r.xs;
         G.rys = r.ys;
     }
+    if (dry) return HG_PYR_STREAM;
     const int op = (even_odd_offset + 1) & 1;   // tap column class at padding 1
     const int fr = from_rect ? 1 : 0;
     if (src_dtype == HG_F16)

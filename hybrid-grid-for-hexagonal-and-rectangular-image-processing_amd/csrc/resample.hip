@@ -541,6 +541,9 @@ int hg_resample_kernel(int op, int sdt, int ddt, int64_t planes, int64_t h, int6
     if (op != HG_OP_RECT_TO_HEX && op != HG_OP_HEX_TO_RECT && op != HG_OP_HEXRESIZE) return HG_EINVAL;
     if (interp == HG_NEAREST && sdt != ddt) return HG_EDTYPE;
     if (interp != HG_NEAREST && interp != HG_LINEAR) return HG_EINVAL;
+    // resample() returns HG_EDTYPE for a non-float linear output (no kernel takes one: the
+    // down kernel's dtype checks decline it first)
+    if (interp == HG_LINEAR && !hg::dtype_is_float(ddt)) return HG_EDTYPE;
     const bool dbl = interp == HG_LINEAR && hg::acc_is_double(sdt, ddt);
     if (op == HG_OP_RECT_TO_HEX && !dbl &&
         hg::down_try(nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, interp, nullptr, true) == HG_OK)

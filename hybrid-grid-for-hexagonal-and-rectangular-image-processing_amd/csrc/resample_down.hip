@@ -307,9 +307,7 @@ static int down_launch(const void* src, void* dst, const DownGeom& D, hipStream_
 
 int down_try(const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h, int64_t w,
              int64_t h1, int64_t w1, int interp, hipStream_t st, bool dry) {
-    if (const char* e = getenv("HYGRID_DOWN")) {    // A/B switch: 0 = general kernels only
-        if (e[0] == '0') return HG_EUNSUP;
-    }
+    if (env_is("HYGRID_DOWN", "0")) return HG_EUNSUP;   // A/B switch: general kernels only
     const bool near = interp == HG_NEAREST;
     int E;
     if (near) {

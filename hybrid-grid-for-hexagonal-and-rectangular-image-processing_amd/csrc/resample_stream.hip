@@ -495,9 +495,7 @@ static bool h2r_exact(const Geom& g, float tri[2][3]) {
 
 int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h,
                int64_t w, int64_t h1, int64_t w1, hipStream_t st, bool dry) {
-    if (const char* e = getenv("HYGRID_STREAM")) {    // A/B switch: 0 = general kernels only
-        if (e[0] == '0') return HG_EUNSUP;
-    }
+    if (env_is("HYGRID_STREAM", "0")) return HG_EUNSUP;   // A/B switch: general kernels only
     if (op != HG_OP_RECT_TO_HEX && op != HG_OP_HEX_TO_RECT) return HG_EUNSUP;
     auto small = [](int dt) { return dt == HG_BF16 || dt == HG_F16 || dt == HG_F32; };
     if (!small(sdt) || !small(ddt)) return HG_EUNSUP;   // f32 accumulator types only

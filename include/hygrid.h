@@ -59,6 +59,8 @@ enum hg_op { HG_OP_RECT_TO_HEX = 0, HG_OP_HEX_TO_RECT = 1, HG_OP_HEXRESIZE = 2 }
 #define HG_EDTYPE (-2)   /* unsupported dtype or dtype combination */
 #define HG_ESHAPE (-3)   /* input too small for the operator / size overflow */
 #define HG_EUNSUP (-4)   /* combination not implemented */
+#define HG_EOVERFLOW (-5) /* a kernel's on-chip tile overflowed (k_pyr_level; not expected:
+                            * the host bounds every tile's footprint before launching) */
 
 int hg_abi_version(void);
 const char* hg_strerror(int status);
@@ -264,6 +266,18 @@ int hg_hex_pyramid_level(const void* x, void* y, int x_dtype, int y_dtype, int64
                          int64_t channels, int64_t h, int64_t w, int64_t h1, int64_t w1,
                          const float* taps, const float* bias, int even_odd_offset,
                          int from_rect, void* stream);
+/* Which kernel hg_hex_pyramid_level would run for this call (nothing is launched):
+ * HG_PYR_FUSED (k_fused MD 3 / 4, pyramid_fused.hip), HG_PYR_FUSED_SHORT (MD 5: the same on
+ * short bands, for levels too small to fill the chip), HG_PYR_STREAM (k_pyr_stream), HG_PYR_LDS
+ * (k_pyr_level, the LDS-tiled fallback), or a negative status.  The environment variable
+ * HYGRID_PYR_KERNEL = "fused" | "stream" | "lds" restricts both calls to that kernel (the
+ * call returns HG_EUNSUP when it cannot run it); for tests and A/B measurements.
+ * The LDS fallback synchronises `stream` once to report HG_EOVERFLOW; the other kernels
+ * never synchronise. */
+enum hg_pyr_kernel { HG_PYR_FUSED = 0, HG_PYR_FUSED_SHORT = 1, HG_PYR_STREAM = 2, HG_PYR_LDS = 3 };
+int hg_hex_pyramid_level_kernel(int x_dtype, int y_dtype, int64_t batch, int64_t channels,
+                                int64_t h, int64_t w, int64_t h1, int64_t w1, int even_odd_offset,
+                                int from_rect);
 
 #ifdef __cplusplus
 }

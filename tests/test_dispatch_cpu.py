@@ -56,3 +56,46 @@ def test_outside_the_domain():
     for op in OPS:
         with pytest.raises(ValueError):
             _abi.resample_kernel(op, _abi.HG_U8, _abi.HG_F32, 1, 8, 8, 4, 4, _abi.HG_NEAREST)
+    # linear needs a floating output, as the launching call (resample() returns HG_EDTYPE)
+    for op in OPS:
+        for dt in (_abi.HG_U8, _abi.HG_I32):
+            with pytest.raises(ValueError, match="dtype"):
+                _abi.resample_kernel(op, _abi.HG_BF16, dt, 1, 64, 64, 64, 64, _abi.HG_LINEAR)
+
+
+def _pyr(*a, **env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return _abi.lib().hg_hex_pyramid_level_kernel(*a)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def test_pyramid_levels_take_the_fused_row_walk():
+    """Config 5's three levels (8 x 3 x 4320 x 7680 fp16: level 0 from the rect image) run
+    on k_fused (MD 3, then MD 4 / MD 5 for levels too small to fill the chip at 60-row bands);
+    HYGRID_PYR_KERNEL restricts the choice (exact values only)."""
+    F16, F32 = _abi.HG_F16, _abi.HG_F32
+    fused = (_abi.HG_PYR_FUSED, _abi.HG_PYR_FUSED_SHORT)
+    assert _pyr(F16, F16, 8, 3, 4320, 7680, 2160, 3840, 0, 1) == _abi.HG_PYR_FUSED
+    assert _pyr(F16, F16, 8, 3, 2160, 3840, 1080, 1920, 0, 0) in fused
+    assert _pyr(F16, F16, 8, 3, 1080, 1920, 540, 960, 0, 0) == _abi.HG_PYR_FUSED_SHORT
+    assert _pyr(F16, F16, 8, 3, 1080, 1920, 540, 960, 0, 0, HYGRID_PYR_SHORT="0") == _abi.HG_PYR_FUSED
+    assert _pyr(F16, F16, 8, 3, 2160, 3840, 1080, 1920, 0, 0,
+                HYGRID_PYR_KERNEL="stream") == _abi.HG_PYR_STREAM
+    assert _pyr(F16, F16, 8, 3, 2160, 3840, 1080, 1920, 0, 0,
+                HYGRID_PYR_KERNEL="lds") == _abi.HG_PYR_LDS
+    # a value that is not exactly a kernel name restricts nothing
+    assert _pyr(F16, F16, 8, 3, 2160, 3840, 1080, 1920, 0, 0, HYGRID_PYR_KERNEL="l") in fused
+    # fp32 levels: only the LDS kernel; restricted to the fused kernel the call declines
+    assert _pyr(F32, F32, 2, 3, 540, 960, 270, 480, 1, 1) == _abi.HG_PYR_LDS
+    assert _pyr(F32, F32, 2, 3, 540, 960, 270, 480, 1, 1,
+                HYGRID_PYR_KERNEL="fused") == _abi.HG_EUNSUP
+    # > 2x downsampling overflows every tile: declined up front by the exact host bound
+    assert _pyr(F32, F32, 1, 3, 540, 960, 100, 180, 0, 0) == _abi.HG_EUNSUP
+    assert _pyr(_abi.HG_U8, F32, 1, 3, 64, 64, 32, 32, 0, 0) == -2   # HG_EDTYPE

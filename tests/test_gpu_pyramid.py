@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():  # pragma: no cover
     pytest.skip("needs a HIP device", allow_module_level=True)
 
-from HyGrid import ops  # noqa: E402
+from HyGrid import _abi, ops  # noqa: E402
 from HyGrid.HexFrames import HexConv2d  # noqa: E402
 from HyGrid.pipeline import hex_pyramid  # noqa: E402
 
@@ -116,31 +116,54 @@ def oracle_levels(x, kern, levels=3):
     return outs
 
 
-def fused_levels_only(x, conv, monkeypatch):
-    """hex_pyramid's fused levels with HYGRID_PYRSTREAM=only: each level must be the
-    row-streaming kernel (level 0 from the rect image), never the LDS fallback."""
-    monkeypatch.setenv("HYGRID_PYRSTREAM", "only")
+def level_kernel(x, size, off=0, from_rect=False, out_dtype=None):
+    """hg_hex_pyramid_level_kernel for this call: the HG_PYR_* kernel that would run, or a
+    negative status (HG_EUNSUP when HYGRID_PYR_KERNEL excludes every kernel that could)."""
+    B, C, h, w = x.shape
+    y_dt = out_dtype or (x.dtype if x.dtype in (torch.float16, torch.bfloat16) else torch.float32)
+    return _abi.lib().hg_hex_pyramid_level_kernel(
+        _abi.dtype_code(x.dtype), _abi.dtype_code(y_dt), B, C, h, w, size[0], size[1], off,
+        int(bool(from_rect)))
+
+
+def run_level_on(kernel, monkeypatch, x, taps, bias, size, off=0, from_rect=False,
+                 out_dtype=None):
+    """One hex_pyramid_level call restricted to `kernel` ("fused" | "stream" | "lds",
+    HYGRID_PYR_KERNEL); returns (HG_PYR_* that ran, output), or (status, None) when that
+    kernel declines the call."""
+    monkeypatch.setenv("HYGRID_PYR_KERNEL", kernel)
     try:
-        H, W = x.shape[-2:]
-        cur, outs, h_, w_ = x, [], H, W
-        with torch.no_grad():
-            for lv in range(3):
-                h_, w_ = h_ // 2, w_ // 2
-                y = ops.hex_pyramid_level(cur, conv.kernel, None, (h_, w_), 0,
-                                          from_rect=(lv == 0), out_dtype=torch.float16)
-                assert y is not None, f"level {lv}: streaming kernel declined {tuple(cur.shape)}"
-                outs.append(y)
-                cur = y
+        k = level_kernel(x, size, off, from_rect, out_dtype)
+        y = ops.hex_pyramid_level(x, taps, bias, size, off, from_rect=from_rect, out_dtype=out_dtype)
     finally:
-        monkeypatch.delenv("HYGRID_PYRSTREAM")
+        monkeypatch.delenv("HYGRID_PYR_KERNEL")
+    assert (k < 0) == (y is None), (kernel, k)
+    return k, y
+
+
+def fused_levels_only(x, conv, monkeypatch):
+    """hex_pyramid's levels restricted to the fused row walk (HYGRID_PYR_KERNEL=fused; level
+    0 k_fused MD 3 from the rect image, levels 1-2 MD 4 / MD 5 from the hex image), each level
+    asserted to be that kernel (hg_hex_pyramid_level_kernel)."""
+    H, W = x.shape[-2:]
+    cur, outs, h_, w_ = x, [], H, W
+    with torch.no_grad():
+        for lv in range(3):
+            h_, w_ = h_ // 2, w_ // 2
+            k, y = run_level_on("fused", monkeypatch, cur, conv.kernel, None, (h_, w_), 0,
+                                from_rect=(lv == 0), out_dtype=torch.float16)
+            assert k in (_abi.HG_PYR_FUSED, _abi.HG_PYR_FUSED_SHORT), f"level {lv}: kernel {k}"
+            outs.append(y)
+            cur = y
     return outs
 
 
 def test_hex_pyramid_8k_fused_full_size(monkeypatch):
     """The bench's config-5 path at full size: hex_pyramid on one 4320x7680 fp16 RGB image
-    (level 0 = k_pyr_stream from the rect image, levels 1-2 streaming) against the oracle
-    with fp64 intermediates and one fp16 rounding per stored level; the streaming kernel is
-    asserted to be what ran (HYGRID_PYRSTREAM=only), and hex_pyramid equals it bit for bit.
+    (level 0 = k_fused MD 3 from the rect image, levels 1-2 MD 4 / MD 5 from the hex image)
+    against the oracle with fp64 intermediates and one fp16 rounding per stored level; the
+    fused kernel is asserted to be what ran, and hex_pyramid (no restriction) equals it bit
+    for bit.
     Tolerance: one fp16 rounding per stored level plus fp32 arithmetic, 3 * 2^-11 of max|ref|."""
     conv = gaussian_conv()
     gen = torch.Generator(device=DEV).manual_seed(5)
@@ -252,25 +275,28 @@ STREAM_CASES = [  # (B, C, h, w): 2x downsamples the row-streaming level kernel 
 @pytest.mark.parametrize("off", [0, 1])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("from_rect", [False, True])
-def test_pyramid_level_stream_vs_oracle_and_lds(case, off, dt, from_rect, monkeypatch):
-    """k_pyr_stream (pyramid_stream.hip: 16-bit, 2x downsample, bands of 30 output rows,
-    windows of 60 output columns) against the fp64 oracle chain within one output rounding
-    of the fp32 result, and against the LDS-tiled k_pyr_level (HYGRID_PYRSTREAM=0) within
-    one output rounding: ragged bands / windows, 1 and 3 channels, both tap classes, bias;
-    from_rect: the level input made on the fly from the rect image (rect_to_hex,
-    geometry_np.py:358-519, same size) against the oracle's r2h -> conv -> hexresize."""
+def test_pyramid_level_kernels_vs_oracle(case, off, dt, from_rect, monkeypatch):
+    """Every level kernel on the 2x downsamples the streaming ones take, each restricted with
+    HYGRID_PYR_KERNEL and asserted to be what ran: k_fused MD 3 / 4 / 5, k_pyr_stream
+    (pyramid_stream.hip) and the LDS-tiled k_pyr_level, each against the fp64 oracle chain
+    within one output rounding of the fp32 result and against each other within two: ragged
+    bands / windows, 1 and 3 channels, both tap classes, bias; from_rect: the level input made
+    on the fly from the rect image (rect_to_hex, geometry_np.py:358-519, same size) against the
+    oracle's r2h -> conv -> hexresize."""
     B, C, h, w = case
     h1, w1 = h // 2, w // 2
     g = torch.Generator().manual_seed(h * 3 + w + off)
     taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
     bias = (torch.rand((C,), generator=g) - 0.5).to(DEV)
     x = torch.rand((B, C, h, w), generator=g).to(DEV).to(dt)
-    monkeypatch.setenv("HYGRID_PYRSTREAM", "only")   # declines instead of falling back
-    y = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=from_rect)
-    monkeypatch.setenv("HYGRID_PYRSTREAM", "0")
-    y_lds = ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=from_rect)
-    monkeypatch.delenv("HYGRID_PYRSTREAM")
-    assert y is not None and y_lds is not None and y.dtype == dt
+    want = {"fused": (_abi.HG_PYR_FUSED, _abi.HG_PYR_FUSED_SHORT), "stream": (_abi.HG_PYR_STREAM,),
+            "lds": (_abi.HG_PYR_LDS,)}
+    ys = {}
+    for name, kinds in want.items():
+        k, y = run_level_on(name, monkeypatch, x, taps, bias, (h1, w1), off, from_rect)
+        assert k in kinds, (name, k)
+        assert y.dtype == dt
+        ys[name] = y
     xd = x.double().cpu().numpy()
     hx = O.rect_to_hex(xd, (h, w), 1).reshape(xd.shape) if from_rect else xd
     c = O.hexconv2d(hx, taps.cpu().double().numpy(), bias.cpu().double().numpy(), off, 2,
@@ -278,32 +304,65 @@ def test_pyramid_level_stream_vs_oracle_and_lds(case, off, dt, from_rect, monkey
     ref = O.hexresize(c, (h1, w1), 1).reshape(B, C, h1, w1)
     ulp = 2.0 ** -8 if dt == torch.bfloat16 else 2.0 ** -11
     scale = float(np.abs(ref).max())
-    got = y.double().cpu().numpy()
-    np.testing.assert_allclose(got, ref, rtol=ulp, atol=ulp * scale)
-    torch.testing.assert_close(y.float(), y_lds.float(), rtol=2 * ulp, atol=2 * ulp * scale)
+    for name, y in ys.items():
+        np.testing.assert_allclose(y.double().cpu().numpy(), ref, rtol=ulp, atol=ulp * scale,
+                                   err_msg=name)
+    for name in ("stream", "lds"):
+        torch.testing.assert_close(ys["fused"].float(), ys[name].float(), rtol=2 * ulp,
+                                   atol=2 * ulp * scale)
+    # the unrestricted call takes the fused kernel and gives its result bit for bit
+    assert level_kernel(x, (h1, w1), off, from_rect) in want["fused"]
+    assert torch.equal(ops.hex_pyramid_level(x, taps, bias, (h1, w1), off, from_rect=from_rect),
+                       ys["fused"])
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float16])
+def test_pyramid_lds_overflow_is_an_error(dt, monkeypatch):
+    """k_pyr_level's footprint overflow is a reported error, not a silent result: with a
+    test-only tile cap of 4 Y rows (HYGRID_PYR_LDS_FORCE_CAP; the host bound is skipped) every
+    tile overflows, the kernel raises the call's fault flag and hg_hex_pyramid_level returns
+    HG_EOVERFLOW (ValueError here).  Without the cap the same call passes the host bound and
+    matches the oracle."""
+    B, C, h, w = 1, 3, 64, 130
+    g = torch.Generator().manual_seed(11)
+    taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
+    x = torch.rand((B, C, h, w), generator=g).to(DEV).to(dt)
+    monkeypatch.setenv("HYGRID_PYR_LDS_FORCE_CAP", "4")
+    with pytest.raises(ValueError, match="overflow"):
+        run_level_on("lds", monkeypatch, x, taps, None, (h // 2, w // 2))
+    monkeypatch.delenv("HYGRID_PYR_LDS_FORCE_CAP")
+    k, y = run_level_on("lds", monkeypatch, x, taps, None, (h // 2, w // 2),
+                        out_dtype=torch.float32)
+    assert k == _abi.HG_PYR_LDS
+    c = O.hexconv2d(x.double().cpu().numpy(), taps.cpu().double().numpy(), None, 0, 2,
+                    padding=1, groups=C)
+    ref = O.hexresize(c, (h // 2, w // 2), 1).reshape(y.shape)
+    tol = 2.0 ** -11 if dt == torch.float16 else 1e-5
+    scale = float(np.abs(ref).max())
+    np.testing.assert_allclose(y.double().cpu().numpy(), ref, rtol=tol, atol=tol * scale)
 
 
 @pytest.mark.parametrize("case", STREAM_CASES + [(8, 3, 1080, 1920)])
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 def test_pyramid_level_short_bands_vs_oracle(case, dt, monkeypatch):
     """A level from a hex image on the fused row walk with 60-row bands (MD 4) and with the
-    short bands small levels take (MD 5, HYGRID_PYR_SHORT=1): bit-identical to each other
-    (a band split changes no output's arithmetic) and within one output rounding of the fp64
-    oracle chain.  (8, 3, 1080, 1920) is the bench's level 2 at full size."""
+    short bands small levels take (MD 5, HYGRID_PYR_SHORT=1), each asserted to be what ran:
+    bit-identical to each other (a band split changes no output's arithmetic) and within one
+    output rounding of the fp64 oracle chain.  (8, 3, 1080, 1920) is the bench's level 2 at
+    full size."""
     B, C, h, w = case
     h1, w1 = h // 2, w // 2
     g = torch.Generator().manual_seed(h + 7 * w)
     taps = (torch.rand((C, 1, 1, 7), generator=g) - 0.3).to(DEV)
     bias = (torch.rand((C,), generator=g) - 0.5).to(DEV)
     x = torch.rand((B, C, h, w), generator=g).to(DEV).to(dt)
-    monkeypatch.setenv("HYGRID_PYRSTREAM", "only")
     outs = []
-    for short in ("0", "1"):
+    for short, kind in (("0", _abi.HG_PYR_FUSED), ("1", _abi.HG_PYR_FUSED_SHORT)):
         monkeypatch.setenv("HYGRID_PYR_SHORT", short)
-        outs.append(ops.hex_pyramid_level(x, taps, bias, (h1, w1), 1))
+        k, y = run_level_on("fused", monkeypatch, x, taps, bias, (h1, w1), 1)
+        assert k == kind
+        outs.append(y)
     monkeypatch.delenv("HYGRID_PYR_SHORT")
-    monkeypatch.delenv("HYGRID_PYRSTREAM")
-    assert outs[0] is not None and outs[1] is not None
     assert torch.equal(outs[0], outs[1])
     n = 1 if B * h * w > 1 << 22 else B          # full-size case: the first image
     xd = x[:n].double().cpu().numpy()

@@ -9,7 +9,7 @@ usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
       hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K, pyr2 = level 2, 2K -> 1K)
   name 'base' = the in-tree library; others = HyGrid/_lib/variants/libhygrid_<name>.so;
   'name%VAR=VAL' runs that library with the environment variable VAR=VAL set around its calls
-  (the library's A/B switches, e.g. base%HYGRID_PYRSTREAM=0)
+  (the library's A/B switches, e.g. base%HYGRID_PYR_KERNEL=lds)
 """
 import ctypes
 import os
