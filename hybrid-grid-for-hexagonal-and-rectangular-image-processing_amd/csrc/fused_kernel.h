@@ -124,6 +124,16 @@ static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
                                       // conv rows in LDS (3 ds_read_b32 per channel at per-lane
                                       // addresses) instead of 5 DPP moves + 9 selects per channel
 #endif
+#ifndef FU_ORDER
+#define FU_ORDER 0                    // workgroup -> (window group, band, image) order (A/B
+                                      // variants; 0: group fastest, then band, then image)
+#endif
+#ifndef FU_LAUX
+#define FU_LAUX 0                     // cache-policy bits of the row loads / stores (A/B variants)
+#endif
+#ifndef FU_SAUX
+#define FU_SAUX 0
+#endif
 #ifndef FU_ODPP
 #define FU_ODPP 1                     // MD 0: the h2r neighbour term as one v_fmac_f32_dpp
 #endif
@@ -167,7 +177,7 @@ template <typename T>
 __device__ __forceinline__ typename RawOf<T>::type fu_load(__amdgpu_buffer_rsrc_t rs,
                                                            unsigned voff, unsigned soff) {
     if constexpr (sizeof(T) == 2) {
-        return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, FU_LAUX);
     } else {
         typedef unsigned u2v __attribute__((ext_vector_type(2)));
         const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
@@ -195,7 +205,7 @@ __device__ __forceinline__ void fu_store(float e, float o, __amdgpu_buffer_rsrc_
     if constexpr (sizeof(T) == 2) {
         typedef T t2v __attribute__((ext_vector_type(2)));
         const t2v p = {(T)e, (T)o};
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, p), rs, voff, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, p), rs, voff, soff, FU_SAUX);
     } else {
         typedef unsigned u2v __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64(
@@ -352,9 +362,13 @@ void k_fused(const Tin* __restrict__ x,
     const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
     const int ngrp = (F.nwin + GW - 1) / GW;
     const int grp = (int)(blk % ngrp);
-    const int64_t rest = blk / ngrp;
-    const int band = (int)(rest % F.nband);
-    const int64_t b = rest / F.nband;
+    int64_t rest = blk / ngrp;
+    if (FU_ORDER == 3) {   // scrambled (band, image) index (40503 is prime to 52 x 128)
+        const int64_t n = (int64_t)F.nband * F.B;
+        rest = (rest * 40503 + 12345) % n;
+    }
+    const int band = (int)(FU_ORDER == 4 ? rest / F.B : rest % F.nband);
+    const int64_t b = FU_ORDER == 4 ? rest % F.B : rest / F.nband;
     if (b >= F.B) return;                         // uniform per workgroup
     const int win = grp * GW + wslot;             // may be >= nwin: runs, owns nothing
     const int W0 = win * FU_OWN - FU_HL;
