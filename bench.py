@@ -174,7 +174,10 @@ def cpu_baseline(args, kernel, bias):
 
 def touched_rows_bytes(ops, op, h, w, h1, w1, dev, nearest, elem):
     """Bytes of the source rows a resample's lattice references (every referenced row is
-    read once, whole: its cache lines are streamed), from the kernel's own integer maps."""
+    read once, whole: its cache lines are streamed), from the kernel's own integer maps.
+    hex -> rect upsampling references every source row: the whole source."""
+    if op != "rect_to_hex":
+        return h * w * elem
     m = ops.lattice_maps(op, h, w, h1, w1, device=dev)
     i_n, valid = m["i_n"].long(), m["valid"].long()
     if nearest:
@@ -196,32 +199,45 @@ def bench_lattices(ops, measure, gen, dev, world, Bl, C, H, W):
     hs, ws = H // 2, W // 2
     xu8 = torch.randint(0, 256, (Bl, C, H, W), generator=gen, device=dev, dtype=torch.uint8)
     xbf = torch.rand((Bl, C, H, W), generator=gen, device=dev, dtype=torch.bfloat16)
+    # the inverse lattice of ConvertToHexagon: a (h//2, w//2) hex image back to the (h, w)
+    # rect raster (hex_to_rect_resample, geometry_np.py:191-356; 'nearest' is
+    # geometry_torch.py:335-347)
+    hu8 = xu8[:, :, :hs, :ws].contiguous()
+    hbf = xbf[:, :, :hs, :ws].contiguous()
     out = {}
-    cases = (("convert_to_hexagon", xu8, 0, 1, "Image.py:111-116: rect->hex (h//2, w//2) nearest, u8"),
-             ("r2h_bilinear_2x", xbf, 1, 2, "geometry_np.py:772-776 ratio: rect->hex (h//2, w//2) bilinear, bf16"))
-    for name, xin, interp, elem, what in cases:
-        def run(record, ev, xin=xin, interp=interp):
+    cases = (("convert_to_hexagon", "rect_to_hex", xu8, 0, 1, (hs, ws),
+              "Image.py:111-116: rect->hex (h//2, w//2) nearest, u8"),
+             ("r2h_bilinear_2x", "rect_to_hex", xbf, 1, 2, (hs, ws),
+              "geometry_np.py:772-776 ratio: rect->hex (h//2, w//2) bilinear, bf16"),
+             ("h2r_linear_2x_up", "hex_to_rect", hbf, 1, 2, (H, W),
+              "geometry_np.py:191-356: hex (h//2, w//2) -> rect (h, w) linear, bf16 (inverse of "
+              "ConvertToHexagon's lattice)"),
+             ("h2r_nearest_2x_up", "hex_to_rect", hu8, 0, 1, (H, W),
+              "geometry_torch.py:335-347: hex (h//2, w//2) -> rect (h, w) nearest, u8"))
+    for name, op, xin, interp, elem, osz, what in cases:
+        def run(record, ev, xin=xin, interp=interp, op=op, osz=osz):
             if record:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 e[0].record()
-            y = ops.rect_to_hex(xin, (hs, ws), interp=interp)
+            y = getattr(ops, op)(xin, osz, interp=interp)
             if record:
                 e[1].record()
                 ev.append(e)
             return y
         steps = 10
         _, el, sms = measure(run, steps)
-        rb = touched_rows_bytes(ops, "rect_to_hex", H, W, hs, ws, dev, interp == 0, elem)
-        alg = Bl * C * (rb + hs * ws * elem)
-        out[name] = {"what": what, "batch_per_gpu": Bl, "in_shape": [Bl, C, H, W],
-                     "out_shape": [Bl, C, hs, ws], "ms": round(sms[0], 4),
-                     "value": round(world * Bl * hs * ws * steps / el / 1e6, 1),
+        hi, wi = int(xin.shape[-2]), int(xin.shape[-1])
+        rb = touched_rows_bytes(ops, op, hi, wi, osz[0], osz[1], dev, interp == 0, elem)
+        alg = Bl * C * (rb + osz[0] * osz[1] * elem)
+        out[name] = {"what": what, "batch_per_gpu": Bl, "in_shape": [Bl, C, hi, wi],
+                     "out_shape": [Bl, C, osz[0], osz[1]], "ms": round(sms[0], 4),
+                     "value": round(world * Bl * osz[0] * osz[1] * steps / el / 1e6, 1),
                      "unit": "Mpix/s (output samples)",
                      "alg_GB": round(alg / 1e9, 4),
-                     "src_rows_referenced_frac": round(rb / (H * W * elem), 4),
+                     "src_rows_referenced_frac": round(rb / (hi * wi * elem), 4),
                      "GB_per_s": round(alg / (sms[0] * 1e-3) / 1e9, 1),
                      "frac_of_peak": round(alg / (sms[0] * 1e-3) / PEAK_BPS, 4)}
-    del xu8, xbf
+    del xu8, xbf, hu8, hbf
     return out
 
 
@@ -484,6 +500,12 @@ def main():
             h_, w_ = h_ // 2, w_ // 2
         unf_bytes *= Bp * C * 2
         names_u = ["rect_to_hex"] + [f"{k}_l{lv}" for lv in range(3) for k in ("hexconv_dw", "hexresize")]
+        # each operator's own bytes (read its input + write its output), for its own fraction
+        own_u, h_, w_ = [2 * Hp * Wp], Hp, Wp
+        for lv in range(3):
+            own_u += [2 * h_ * w_, h_ * w_ + (h_ // 2) * (w_ // 2)]
+            h_, w_ = h_ // 2, w_ // 2
+        own_u = [Bp * C * 2 * v for v in own_u]
         pyramid = {"workload": "config5: 8K RGB fp16, r2h -> 3 x [depthwise Gaussian HexConv2d "
                                "-> hexresize /2]",
                    "path": "hg_hex_pyramid_level x 3 (conv + hexresize, fp32 on chip; level 0 "
@@ -500,7 +522,10 @@ def main():
                    "unfused": {"ms_per_step": round(el_pu / steps_p * 1e3, 4),
                                "alg_GB": round(unf_bytes / 1e9, 4),
                                "frac_of_peak": round(unf_bytes / (el_pu / steps_p) / PEAK_BPS, 4),
-                               "kernels_ms": {k: round(m, 4) for k, m in zip(names_u, sms_pu)}}}
+                               "kernels_ms": {k: round(m, 4) for k, m in zip(names_u, sms_pu)},
+                               "kernels": {k: {"ms": round(m, 4), "alg_GB": round(b / 1e9, 4),
+                                               "frac_of_peak": round(b / (m * 1e-3) / PEAK_BPS, 4)}
+                                           for k, m, b in zip(names_u, sms_pu, own_u)}}}
         del xp
 
     roundtrip = None

@@ -258,6 +258,11 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16(const __bf16* 
             }
         }
         // ---- stage the weights of taps (o, t), 8 channels, as 3 bf16 parts ----------------
+        // (ml: some weight of the chunk needs its second / third part; when none does, the
+        // pt = 1, 2 passes are skipped: half the MFMA work for bf16-exact weights, and an
+        // infinite input times a weight then stays +-Inf as in one fp32 product instead of
+        // meeting a zero part as Inf * 0 = NaN)
+        int ml = 0;
         for (int e = tid; e < CM_O * 8; e += CM_THREADS) {
             const int o = e >> 3, t = e & 7, og = o0 + o;
             unsigned short h[8], m[8], l[8];
@@ -272,6 +277,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16(const __bf16* 
                 h[cc] = __builtin_bit_cast(unsigned short, bh);
                 m[cc] = __builtin_bit_cast(unsigned short, bm);
                 l[cc] = __builtin_bit_cast(unsigned short, bl);
+                ml |= (m[cc] | l[cc]) & 0x7fff;              // a nonzero part (+-0 is zero)
             }
             const int kb = t >> 2, g = t & 3;
             auto pk = [](const unsigned short* u) {
@@ -282,7 +288,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16(const __bf16* 
             wsb[((1 * 2 + kb) * CM_O + o) * 4 + g] = pk(m);
             wsb[((2 * 2 + kb) * CM_O + o) * 4 + g] = pk(l);
         }
-        __syncthreads();
+        const int nparts = __syncthreads_or(ml != 0) ? 3 : 1;   // uniform per workgroup
         // ---- 2 k blocks x 4 column tiles x 3 weight parts x NOT channel tiles -------------
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
@@ -292,6 +298,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16(const __bf16* 
                 bf[qt] = __builtin_bit_cast(cm_b8, psb[pidx[kb] < 0 ? CB_PSZ - 1 : pidx[kb] + qt * 16]);
 #pragma unroll
             for (int pt = 0; pt < 3; ++pt) {
+                if (pt >= nparts) break;
 #pragma unroll
                 for (int ot = 0; ot < NOT; ++ot) {
                     const cm_b8 af = __builtin_bit_cast(cm_b8, wsb[((pt * 2 + kb) * CM_O + ot * 16 + li) * 4 + lg]);

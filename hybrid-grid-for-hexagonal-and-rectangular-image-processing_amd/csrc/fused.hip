@@ -43,7 +43,7 @@ namespace hg {
 template <typename Tin, typename Tout, int C, int O, int G>
 static int fused_launch(const void* x, const float* k, const float* bias, void* y,
                         const FusedGeom& F, int op, hipStream_t st) {
-    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + 3) / 4);
+    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + FU_GW - 1) / FU_GW);
     if (blocks > INT_MAX) return HG_ESHAPE;
     const dim3 grid((unsigned)blocks), blk(FU_THREADS);
     if (op)
@@ -101,7 +101,7 @@ int fused_rt_try(const void* x, void* y, int x_dtype, int y_dtype, int64_t plane
     F.rys = g.ys;
     F.nwin = (int)((w1 + FU_OWN - 1) / FU_OWN);
     F.nband = (int)((h1 + fu_rb(2) - 1) / fu_rb(2));
-    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + 3) / 4);
+    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + FU_GW - 1) / FU_GW);
     if (blocks > INT_MAX) return HG_ESHAPE;
     const dim3 grid((unsigned)blocks), blk(FU_THREADS);
 #define HG_RT(TI, TO)                                                                          \

@@ -14,7 +14,7 @@ namespace hg {
 template <typename Tin, typename Tout, int C, int O, int G>
 static int fconv_launch(const void* x, const float* k, const float* bias, void* y,
                         const FusedGeom& F, int op, hipStream_t st) {
-    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + 3) / 4);
+    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + FU_GW - 1) / FU_GW);
     if (blocks > INT_MAX) return HG_ESHAPE;
     const dim3 grid((unsigned)blocks), blk(FU_THREADS);
     if (op)

@@ -13,7 +13,11 @@
 
 namespace hg {
 
-constexpr int FU_THREADS = 256;       // 4 independent waves per workgroup
+#ifndef FU_GW_
+#define FU_GW_ 4
+#endif
+constexpr int FU_GW = FU_GW_;          // waves (adjacent windows) per workgroup
+constexpr int FU_THREADS = 64 * FU_GW;
 #ifndef FU_HL_
 #define FU_HL_ 4
 #endif
@@ -123,6 +127,18 @@ static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
 #define FU_PLDS 1                     // MD 3 / 4: the triangle vertices read from the wave's two
                                       // conv rows in LDS (3 ds_read_b32 per channel at per-lane
                                       // addresses) instead of 5 DPP moves + 9 selects per channel
+#endif
+#ifndef FU_DMA
+#define FU_DMA 0                      // MD 0, 16-bit input: rect rows arrive by LDS-DMA as
+                                      // workgroup-wide 1-KiB row pieces (one per plane, issued by
+                                      // waves 0..C-1), a ring of rows in LDS, one s_barrier per step
+#endif
+#ifndef FU_DMA_ST
+#define FU_DMA_ST 1                   // with FU_DMA and 16-bit outputs: output rows staged in LDS
+                                      // and stored as the workgroup's 960-B row pieces (16-B lanes)
+#endif
+#ifndef FU_DPD
+#define FU_DPD 3                      // with FU_DMA: rect rows in flight ahead of the one read
 #endif
 #ifndef FU_ORDER
 #define FU_ORDER 0                    // workgroup -> (window group, band, image) order (A/B
@@ -344,8 +360,25 @@ void k_fused(const Tin* __restrict__ x,
     constexpr bool STAGE = FU_STAGE && sizeof(Tout) == 2;
     constexpr int GW = FU_THREADS / 64;             // windows per group
     constexpr int GDW = GW * FU_OWN / 2;            // dwords of one output row of a group
+    // DMA: ring of NSR rect rows, each C planes x the group's 1-KiB span (columns
+    // grp * GW * FU_OWN - 8 .. + 511); DST: two output rows, O planes x 256 dwords.  With DMA
+    // the row tables, the ring and the staged rows share ONE __shared__ array: LDS accesses
+    // to a second __shared__ object make hipcc wait vmcnt(0) for every LDS-DMA in flight.
+    // P: 1-KiB pieces per plane row of the group (GW windows of FU_OWN columns + halo)
+    constexpr int DP = (GW * FU_OWN + 16 + 511) / 512;
+    constexpr bool DMA = FU_DMA && MD == 0 && sizeof(Tin) == 2 && GW >= C * DP;
+    constexpr bool DST = DMA && FU_DMA_ST && sizeof(Tout) == 2 && GW >= O * DP;
+    constexpr int DPD = FU_DPD, NSR = DPD + 6;
+    static_assert(!(DMA && (FU_STAGE || FU_NOMEM)), "FU_DMA replaces FU_STAGE / FU_NOMEM");
+    constexpr int DLUT = GW * FU_LUT * 16, DRING = NSR * C * DP * 1024, DSTGB = DST ? 2 * O * DP * 1024 : 0;
+    __shared__ __attribute__((aligned(16))) unsigned char dsm[DMA ? DLUT + DRING + DSTGB : 16];
+    unsigned char* const dring = dsm + DLUT;
+    // the ring's LDS byte address (the M0 base of an LDS-DMA), from the array itself
+    const unsigned dring_lds =
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)dsm + (unsigned)DLUT;
+    unsigned* const dstg = reinterpret_cast<unsigned*>(dsm + DLUT + DRING);
     // per-wave u-row table {a, b, c, -}: u[r] = a*x[r-1] + b*x[r] + c*x[r+1]
-    __shared__ float4 lut_all[GW][FU_LUT];
+    __shared__ float4 lut_all[DMA ? 1 : GW][FU_LUT];
     __shared__ unsigned stg[STAGE ? 2 : 1][STAGE ? 6 : 1][STAGE ? O : 1][STAGE ? GDW + 4 : 1];
     // PLDS: the two conv rows an output row reads, per wave: [row][channel][col], cols
     // 0..127 of the window + a zero at 128 (vertices outside the raster) and a pad
@@ -354,7 +387,7 @@ void k_fused(const Tin* __restrict__ x,
     __shared__ float zl_all[PLDS ? GW : 1][PLDS ? 2 * O * ZW : 1];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float4* lut = lut_all[wslot];
+    float4* lut = DMA ? reinterpret_cast<float4*>(dsm) + wslot * FU_LUT : lut_all[DMA ? 0 : wslot];
     float* zl = zl_all[PLDS ? wslot : 0];
     if constexpr (PLDS) {
         if (lane < 2 * O) zl[lane * ZW + 128] = 0.f;   // the zero vertex of every row block
@@ -469,6 +502,24 @@ void k_fused(const Tin* __restrict__ x,
         if (FU_NOMEM) return 0u;
         return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(k, 0), F.h - 1) * xrow));
     };
+    // DMA: the group's span of a rect row starts 8 columns left of the group (16-B aligned)
+    // and is DP 1-KiB pieces; wave j < C * DP moves piece j % DP of plane j / DP, lane l 8
+    // columns (16 B) of it; columns outside the raster read as zeros
+    const int dcol0 = grp * GW * FU_OWN - 8;
+    const int dpl = wslot / DP, dpp = wslot % DP;      // this wave's plane / piece
+    const int dgc = dcol0 + dpp * 512 + 8 * lane;
+    const unsigned dvoff = (dgc >= 0 && dgc < F.w) ? (unsigned)dgc * 2u : 0x80000000u;
+    const int dlcol = 2 * (ce - dcol0);                 // this lane's column pair in the span
+    // DST: wave j < O * DP stores part j % DP (960 owned bytes, 16 B per lane) of plane j / DP
+    // of the group's output row
+    const int dscol = grp * GW * FU_OWN + dpp * 480 + 8 * lane;
+    const unsigned dsoff = (lane < 60 && dscol < F.w2) ? (unsigned)dscol * 2u : 0x80000000u;
+    // a part whose last 16-B piece crosses the raster's right edge (w2 % 8 != 0) stores as dwords
+    const bool dedge = (F.w2 & 7) != 0 && grp * GW * FU_OWN + dpp * 480 < F.w2 &&
+                       grp * GW * FU_OWN + dpp * 480 + 480 > F.w2;
+    // this lane's dword in a staged output row (pad dwords past the owned ones otherwise)
+    const int dsidx = (lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2)
+                          ? wslot * (FU_OWN / 2) + lane - FU_HL / 2 : GW * (FU_OWN / 2) + (lane & 3);
 
     // ---- weights and bias in VGPRs -------------------------------------------------
     // A VALU instruction with an SGPR (or literal) operand issues at half rate on gfx950
@@ -539,6 +590,7 @@ void k_fused(const Tin* __restrict__ x,
         constexpr int RC = decltype(RCc)::value;
         // ---- state -----------------------------------------------------------------
         Raw raw[6][C];                      // rect rows in flight, slot (row - s0) % 6
+        Raw rawn[C];                        // DMA: the next rect row, read from the LDS ring
         fu_f2 XP[3][C];                     // rect rows as f32 (even, odd) pairs, slot (row - s0) % 3
         float ZE[3][O], ZO[3][O];           // conv rows being accumulated, slot (row - s0) % 3
         constexpr bool PK = FU_PK && MD != 2;
@@ -556,6 +608,51 @@ void k_fused(const Tin* __restrict__ x,
             constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
     #pragma unroll
             for (int c = 0; c < C; ++c) XP[XS][c] = fu_unpack2<Tin>(raw[RS][c], hi16);
+        };
+        // DMA: rect row R lives in ring slot (R - s0 + 2) % NSR; waves 0 .. C-1 each move one
+        // plane's 1-KiB piece of it (uniform branch), every wave reads its column pair
+        auto dslot = [&](int R) { return (R - s0 + 2) % NSR; };
+        // (inline asm: hipcc does not see these loads, so it inserts no vmcnt(0) before the
+        // kernel's other LDS accesses; the waits are counted by hand below)
+        auto dma_row = [&](int R) {
+            if (wslot < C * DP) {
+                const unsigned so = row_off(R) + (unsigned)dpl * xplane;
+                const unsigned lda = dring_lds + (unsigned)(((dslot(R) * C + dpl) * DP + dpp) * 1024);
+                unsigned keep;
+                const unsigned vo = dvoff;          // (asm operands: locals of this lambda)
+                const __amdgpu_buffer_rsrc_t rs = xrs;
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                             "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(vo), "s"(rs), "s"(lda), "s"(so) : "memory");
+            }
+        };
+        auto read_row = [&](int R, Raw (&r)[C]) {
+            const unsigned char* const src = dring + dslot(R) * C * DP * 1024 + dlcol;
+    #pragma unroll
+            for (int c = 0; c < C; ++c) r[c] = *reinterpret_cast<const Raw*>(src + c * DP * 1024);
+        };
+        // DST: output row R (staged at the previous step, buffer R & 1) as the group's 960-B
+        // pieces, wave o storing plane o; `valid` false: a dropped store (keeps the wait count)
+        auto dst_store = [&](int R, bool valid) {
+            if (wslot < O * DP) {
+                const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)max(R, 0) * yrow)) +
+                                    (unsigned)dpl * yplane;
+                const unsigned* const src =
+                    dstg + ((R & 1) * O + dpl) * DP * 256 + dpp * 240 + 4 * min(lane, 59);
+                if (!dedge) {
+                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                    const u4v q = *reinterpret_cast<const u4v*>(src);
+                    __builtin_amdgcn_raw_buffer_store_b128(q, yrs, valid ? dsoff : 0x80000000u, so, 0);
+                } else {   // the row end crosses a 16-B piece: dword stores, column-checked
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const bool in_ = valid && lane < 60 && dscol + 2 * i < F.w2;
+                        __builtin_amdgcn_raw_buffer_store_b32(src[i], yrs,
+                                                              in_ ? (unsigned)(dscol + 2 * i) * 2u : 0x80000000u,
+                                                              so, 0);
+                    }
+                }
+            }
         };
 
         // u row r (= s0 + PH + 1) from rect rows r-1, r, r+1 (ring slots PH, PH+1, PH+2
@@ -829,6 +926,14 @@ void k_fused(const Tin* __restrict__ x,
                 float e2 = ZP[S0][2].x, o2 = ZP[S0][2].y;
                 if constexpr ((PH & 1) == 0) fu_h2r3_even(e0, o0, e1, o1, e2, o2, c13, wn_f);
                 else fu_h2r3_odd(e0, o0, e1, o1, e2, o2, c13, wp_f);
+                if constexpr (DST) {                // staged: stored at the next step
+                    typedef Tout t2v __attribute__((ext_vector_type(2)));
+                    unsigned* const d = dstg + (a2 & 1) * O * DP * 256 + dsidx;
+                    d[0] = __builtin_bit_cast(unsigned, t2v{(Tout)e0, (Tout)o0});
+                    d[DP * 256] = __builtin_bit_cast(unsigned, t2v{(Tout)e1, (Tout)o1});
+                    d[2 * DP * 256] = __builtin_bit_cast(unsigned, t2v{(Tout)e2, (Tout)o2});
+                    return;
+                }
                 fu_store<Tout>(e0, o0, yrs, yoff, so);
                 fu_store<Tout>(e1, o1, yrs, yoff, so + yplane);
                 fu_store<Tout>(e2, o2, yrs, yoff, so + 2 * yplane);
@@ -854,7 +959,10 @@ void k_fused(const Tin* __restrict__ x,
                     oe = fmaf(wp_e, f_prev(zo), c75 * ze);
                     oo = fmaf(c25, ze, c75 * zo);
                 }
-                    if constexpr (STAGE) {
+                    if constexpr (DST) {
+                    typedef Tout t2v __attribute__((ext_vector_type(2)));
+                    dstg[((a2 & 1) * O + o) * DP * 256 + dsidx] = __builtin_bit_cast(unsigned, t2v{(Tout)oe, (Tout)oo});
+                } else if constexpr (STAGE) {
                     typedef Tout t2v __attribute__((ext_vector_type(2)));
                     const t2v pk = {(Tout)oe, (Tout)oo};
                     stg[SB][PH][o][sidx] = __builtin_bit_cast(unsigned, pk);
@@ -896,6 +1004,29 @@ void k_fused(const Tin* __restrict__ x,
         };
 
         // ---- prologue: u rows s0-1 and s0 -------------------------------------------
+        if constexpr (DMA) {
+            // rect rows s0-2 .. s0+2+DPD into the ring, drained and published to the group
+            for (int R = s0 - 2; R <= s0 + 2 + DPD; ++R) dma_row(R);
+            __builtin_amdgcn_s_waitcnt(0x0f70);                     // vmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            Raw t0[C], t1[C], t2[C];
+            read_row(s0 - 2, t0);
+            read_row(s0 - 1, t1);
+            read_row(s0, t2);
+    #pragma unroll
+            for (int c = 0; c < C; ++c) {
+                XP[1][c] = fu_unpack2<Tin>(t0[c], hi16);   // row s0-2 -> slot 1
+                XP[2][c] = fu_unpack2<Tin>(t1[c], hi16);   // row s0-1 -> slot 2
+                XP[0][c] = fu_unpack2<Tin>(t2[c], hi16);   // row s0   -> slot 0
+            }
+            urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});   // u row s0-1: above only
+            read_row(s0 + 1, t0);
+    #pragma unroll
+            for (int c = 0; c < C; ++c) XP[1][c] = fu_unpack2<Tin>(t0[c], hi16);   // row s0+1
+            urow(IC<-1>{}, lut[1], std::true_type{}, std::false_type{});    // u row s0: above, centre
+            read_row(s0 + 2, rawn);
+        } else {
         {
             Raw t0[C], t1[C], t2[C];
             const unsigned o0 = row_off(s0 - 2), o1 = row_off(s0 - 1), o2 = row_off(s0);
@@ -928,6 +1059,7 @@ void k_fused(const Tin* __restrict__ x,
         // entry path with the back edge, and a ring load issued late on the entry path would
         // otherwise put a near-zero vmcnt wait into every iteration.
         if (FU_DRAIN) __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+        }
 
         // ---- main loop ---------------------------------------------------------------
         float4 lnext = lut[2];
@@ -936,8 +1068,27 @@ void k_fused(const Tin* __restrict__ x,
             // keep each step's instructions inside the step: across a 12-step body the
             // scheduler otherwise hoists loads many steps ahead (266 VGPRs, 1 wave / SIMD)
             if (FU_SCHED) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (DMA) {
+                dma_row(a2 + 3 + DPD);
+                // this wave's piece of row a2+3 landed once at most the operations issued after
+                // it are outstanding: DPD steps of (1 piece + the step's stores) (vmcnt counts
+                // loads, stores and LDS-DMA together, in issue order); then the group's barrier
+                // publishes every piece of the row (and orders the staged row's reads)
+                constexpr int N = DPD * (1 + (DST ? 1 : O));
+                static_assert(N < 64, "vmcnt");
+                // + lgkmcnt(0): this wave's staged row (LDS writes of the previous step) is in
+                // LDS before the barrier lets the storing waves read it
+                __builtin_amdgcn_s_waitcnt(0x0070 | (N & 0xf) | ((N >> 4) << 14));
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+    #pragma unroll
+                for (int c = 0; c < C; ++c) XP[(PH + 2) % 3][c] = fu_unpack2<Tin>(rawn[c], hi16);   // row a2+2
+                read_row(a2 + 3, rawn);
+                if constexpr (DST) dst_store(a2 - 1, a2 > s0);
+            } else {
             convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row a2+2
             issue(IC<(PH + 2 + PD) % 6>{}, a2 + 2 + PD);
+            }
             const float4 L = lnext;
             lnext = lut[min(a2 - s0 + 3, NLUT - 1)];
             urow(PHc, L, std::true_type{}, std::true_type{});           // u row a2+1
@@ -986,6 +1137,12 @@ void k_fused(const Tin* __restrict__ x,
             tail(IC<1>{}, base + 6);
         } else {
             tail(IC<0>{}, base);
+        }
+        if constexpr (DST) {                        // the band's last output row
+            __builtin_amdgcn_s_waitcnt(0xc07f);     // lgkmcnt(0): this wave's staged row
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            dst_store(s1 - 1, true);
         }
     };
     if constexpr (UIN) {

@@ -506,6 +506,10 @@ static int resample(const void* src, void* dst, int sdt, int ddt, int64_t planes
         const int rc = stream_try(OP, src, dst, sdt, ddt, planes, h, w, h1, w1, s);
         if (rc != HG_EUNSUP) return rc;
     }
+    if (!dbl && OP != OP_R2H) {      // ~2x hexresize (pyramid levels), 2x up hex -> rect
+        const int rc = tristream_try(OP, src, dst, sdt, ddt, planes, h, w, h1, w1, s, false);
+        if (rc != HG_EUNSUP) return rc;
+    }
     HG_DISPATCH_IN(sdt, TIN, HG_DISPATCH_FLOAT_OUT(ddt, TOUT, {
         if (dbl) return launch_linear<OP, TIN, TOUT, double>(src, dst, planes, g, s);
         return launch_linear<OP, TIN, TOUT, float>(src, dst, planes, g, s);
@@ -552,6 +556,9 @@ int hg_resample_kernel(int op, int sdt, int ddt, int64_t planes, int64_t h, int6
     if (!dbl && op != HG_OP_HEXRESIZE &&
         hg::stream_try(op, nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, nullptr, true) == HG_OK)
         return HG_KERNEL_STREAM;
+    if (!dbl && op != HG_OP_RECT_TO_HEX && interp == HG_LINEAR &&
+        hg::tristream_try(op, nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, nullptr, true) == HG_OK)
+        return HG_KERNEL_DOWN;
     return HG_KERNEL_GENERAL;
 }
 

@@ -15,6 +15,11 @@ int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t pla
 
 // ~2x downsampling rect->hex (ConvertToHexagon's (h//2, w//2) 'nearest' on 8/16-bit data, the
 // demo's bilinear on bf16/f16; resample_down.hip); HG_EUNSUP (nothing launched) otherwise.
+// hexresize_down.hip: triangle-blend resamples (op HG_OP_HEXRESIZE / HG_OP_HEX_TO_RECT,
+// linear, 16-bit in) whose vertices for a run of output columns fit a 128-column input
+// window (~2x hexresize: the pyramid levels; hex (h/2, w/2) -> rect (h, w)); HG_EUNSUP otherwise
+int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h,
+                  int64_t w, int64_t h1, int64_t w1, hipStream_t st, bool dry);
 int down_try(const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h, int64_t w,
              int64_t h1, int64_t w1, int interp, hipStream_t st, bool dry = false);
 

@@ -109,7 +109,8 @@ int hg_resample_backward(int op, const void* gy, void* dx, int acc_dtype, int64_
 /* Which kernel hg_rect_to_hex / hg_hex_to_rect / hg_hexresize would run for this call
  * (nothing is launched): HG_KERNEL_GENERAL (k_resample_lds / k_resample_direct),
  * HG_KERNEL_NEAREST (k_resample_nearest), HG_KERNEL_STREAM (near-identity row streaming,
- * resample_stream.hip), HG_KERNEL_DOWN (~2x downsampling rect->hex, resample_down.hip), or a
+ * resample_stream.hip), HG_KERNEL_DOWN (~2x downsampling streaming kernels: rect->hex,
+ * resample_down.hip; hexresize (pyramid levels), hexresize_down.hip), or a
  * negative status.  Introspection for tests and tools; the reference has no counterpart. */
 enum hg_kernel { HG_KERNEL_GENERAL = 0, HG_KERNEL_NEAREST = 1, HG_KERNEL_STREAM = 2,
                  HG_KERNEL_DOWN = 3 };

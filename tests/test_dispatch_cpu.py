@@ -41,8 +41,33 @@ def test_same_size_keeps_its_kernels():
     for op in (_abi.HG_OP_RECT_TO_HEX, _abi.HG_OP_HEX_TO_RECT):
         assert _kernel(op, _abi.HG_BF16, _abi.HG_BF16, 3, 2160, 3840, 2160, 3840,
                        _abi.HG_LINEAR) == _abi.HG_KERNEL_STREAM
-    assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 4320, 7680, 2160, 3840,
+    # hexresize at the pyramid's 2x ratio: the streaming hexresize kernel (hexresize_down.hip);
+    # fp32 in, fp64 out (the NumPy API's bit-exact path) and 4x keep the general kernel
+    for h, w in ((4320, 7680), (2160, 3840), (1080, 1920), (35, 126), (9, 22)):
+        for dt, ot in ((_abi.HG_F16, _abi.HG_F16), (_abi.HG_BF16, _abi.HG_F32)):
+            assert _kernel(_abi.HG_OP_HEXRESIZE, dt, ot, 24, h, w, h // 2, w // 2,
+                           _abi.HG_LINEAR) == _abi.HG_KERNEL_DOWN
+        assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 24, h, w, h // 2, w // 2,
+                       _abi.HG_LINEAR, HYGRID_DOWN="0") == _abi.HG_KERNEL_GENERAL
+    for dt, ot in ((_abi.HG_F32, _abi.HG_F32), (_abi.HG_F16, _abi.HG_F64)):
+        assert _kernel(_abi.HG_OP_HEXRESIZE, dt, ot, 3, 2160, 3840, 1080, 1920,
+                       _abi.HG_LINEAR) == _abi.HG_KERNEL_GENERAL
+    # odd input widths (rows not dword-aligned for LDS-DMA) keep the general kernel
+    assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 33, 125, 16, 62,
                    _abi.HG_LINEAR) == _abi.HG_KERNEL_GENERAL
+    # any ratio whose window of >= 16 output columns keeps its vertices in 128 input columns
+    # (4x: 30 columns per wave); 16x does not fit
+    assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 2160, 3840, 540, 960,
+                   _abi.HG_LINEAR) == _abi.HG_KERNEL_DOWN
+    assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 2160, 3840, 135, 240,
+                   _abi.HG_LINEAR) == _abi.HG_KERNEL_GENERAL
+    # hex (h/2, w/2) -> rect (h, w), the inverse of ConvertToHexagon's lattice: the same
+    # streaming triangle kernel (two output columns per lane); fp64 out keeps the general one
+    for h, w in ((2160, 3840), (540, 964), (1080, 1920)):
+        assert _kernel(_abi.HG_OP_HEX_TO_RECT, _abi.HG_BF16, _abi.HG_BF16, 96, h // 2, w // 2, h,
+                       w, _abi.HG_LINEAR) == _abi.HG_KERNEL_DOWN
+        assert _kernel(_abi.HG_OP_HEX_TO_RECT, _abi.HG_BF16, _abi.HG_F64, 96, h // 2, w // 2, h,
+                       w, _abi.HG_LINEAR) == _abi.HG_KERNEL_GENERAL
 
 
 def test_outside_the_domain():

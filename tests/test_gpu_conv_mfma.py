@@ -202,3 +202,26 @@ def test_mfma_bf16_nan_positions_match_generic():
     assert torch.equal(torch.isnan(ref) & ~torch.isnan(y), torch.zeros_like(y, dtype=torch.bool))
     fin = torch.isfinite(ref)
     torch.testing.assert_close(y[fin], ref[fin], rtol=1e-5, atol=1e-5 * float(ref[fin].abs().max()))
+
+
+def test_mfma_bf16_exact_weights_keep_inf():
+    """Weights exactly representable in bf16 (Gaussian-style taps 1/4, 1/8, ..., and zeros):
+    every chunk's second and third weight parts are 0, so the kernel runs only the first
+    part's MFMAs (conv_mfma.hip: nparts) and an infinite input times a weight stays +-Inf,
+    exactly as the generic kernel's fp32 products: the same NaN and Inf positions and signs,
+    finite outputs within 1e-5."""
+    B, C, O_, h, w = 1, 16, 16, 20, 70
+    g = torch.Generator().manual_seed(21)
+    k = (torch.randint(-4, 5, (O_, C, 1, 7), generator=g).float() / 8.0).to(DEV)
+    b = (torch.randint(-4, 5, (O_,), generator=g).float() / 4.0).to(DEV)
+    x = _bf16_input((B, C, h, w), 9)
+    x[0, 3, 0, 5] = float("nan")
+    x[0, 7, 19, 69] = float("inf")
+    x[0, 9, 10, 30] = float("-inf")
+    y = ops.hexconv2d(x, k, b, 1, 2, padding=1, out_dtype=torch.float32)
+    ref = _generic(ops.hexconv2d, x, k, b, 1, 2, padding=1, out_dtype=torch.float32)
+    assert torch.equal(torch.isnan(y), torch.isnan(ref))
+    assert torch.equal(torch.isinf(y), torch.isinf(ref))
+    assert torch.equal(y[torch.isinf(ref)], ref[torch.isinf(ref)])
+    fin = torch.isfinite(ref)
+    torch.testing.assert_close(y[fin], ref[fin], rtol=1e-5, atol=1e-5 * float(ref[fin].abs().max()))

@@ -91,7 +91,7 @@ def test_nearest_16bit(h, w, dt):
     _same_bits(y, _general(ops.rect_to_hex, x, size, interp=_abi.HG_NEAREST))
 
 
-@pytest.mark.parametrize("out", [None, torch.float32])
+@pytest.mark.parametrize("out", [None, torch.float32, torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("h,w,size", [(9, 22, (4, 11)), (64, 66, (32, 33)), (512, 683, (256, 341)),
                                       (130, 2050, (65, 1025)), (100, 1000, (50, 500)),
@@ -111,8 +111,9 @@ def test_bilinear_2x(h, w, size, dt, out):
         scale = np.abs(ref).max()
         if out == torch.float32:
             np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5 * scale)
-        else:   # one 16-bit rounding of an fp32 result
-            ulp = 2.0 ** (-8 if dt == torch.bfloat16 else -11)
+        else:   # one 16-bit rounding of an fp32 result (in the output's dtype)
+            od = dt if out is None else out
+            ulp = 2.0 ** (-8 if od == torch.bfloat16 else -11)
             assert np.abs(got - ref).max() <= ulp * scale
 
 

@@ -6,7 +6,9 @@ min per launch and the median per-round ratio to the first variant named).
 usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
   OP: r2h | h2r | conv | wide (HexConv2d 64->64, 1080p bf16 b4) | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1 | pyr2   (bf16 4K b128 for
       r2h/h2r/conv; fp32 1080p b32 for r2h32/h2r32 and rt, the fused round trip; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K from a
-      hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K, pyr2 = level 2, 2K -> 1K)
+      hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K, pyr2 = level 2, 2K -> 1K;
+      hr0 / hr1 / hr2 = hexresize alone at those three levels (fp16); up = hex (h/2, w/2) -> rect (h, w)
+      linear at 4K bf16 b32, the inverse of ConvertToHexagon's lattice)
   name 'base' = the in-tree library; others = HyGrid/_lib/variants/libhygrid_<name>.so;
   'name%VAR=VAL' runs that library with the environment variable VAR=VAL set around its calls
   (the library's A/B switches, e.g. base%HYGRID_PYR_KERNEL=lds)
@@ -47,15 +49,19 @@ def main():
         B, C, H, W, t = 32, 3, 1080, 1920, torch.float32
     elif op == "wide":
         B, C, H, W, t = 4, 64, 1080, 1920, torch.bfloat16
-    elif op == "pyr1":
+    elif op in ("pyr1", "hr1"):
         B, C, H, W, t = 8, 3, 2160, 3840, torch.float16
-    elif op == "pyr2":
+    elif op in ("pyr2", "hr2"):
         B, C, H, W, t = 8, 3, 1080, 1920, torch.float16
+    elif op == "up":
+        B, C, H, W, t = 32, 3, 1080, 1920, torch.bfloat16
     else:
         B, C, H, W, t = 8, 3, 4320, 7680, torch.float16
     x = torch.rand((B, C, H, W), generator=g, device=dev, dtype=t)
-    if op.startswith("pyr"):
+    if op.startswith("pyr") or op.startswith("hr"):
         y = torch.empty((B, C, H // 2, W // 2), device=dev, dtype=t)
+    elif op == "up":
+        y = torch.empty((B, C, 2 * H, 2 * W), device=dev, dtype=t)
         taps = (torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32, device=dev) / 12).repeat(C)
     else:
         y = torch.empty_like(x)
@@ -77,6 +83,14 @@ def main():
             f = lib.hg_pipeline_r2h_h2r
             f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_vp]
             return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, H, W, s)
+        if op.startswith("hr"):
+            f = lib.hg_hexresize
+            f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_int, _vp]
+            return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, H // 2, W // 2, 1, s)
+        if op == "up":
+            f = lib.hg_hex_to_rect
+            f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_int, _vp]
+            return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, 2 * H, 2 * W, 1, s)
         if op in ("conv", "wide"):
             f = lib.hg_hexconv2d
             f.argtypes = [_vp] * 4 + [_int] * 3 + [_i64] * 5 + [_int] * 7 + [_dbl, _vp]

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-4 GPU session A: new parity tests (streaming triangle kernel, pyramid kernel
+# selection / overflow, bf16-exact MFMA weights, cross-dtype r2h down), then A/Bs.
+set -o pipefail
+OUT=gpurun_out/r04a; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+    tests/test_gpu_hexdown.py tests/test_gpu_pyramid.py tests/test_gpu_conv_mfma.py tests/test_gpu_down.py \
+    > $OUT/pytest.log 2>&1; rc=$?
+tail -15 $OUT/pytest.log
+[ $rc -eq 0 ] || exit $rc
+for op in hr0 hr1 hr2 up; do
+  timeout -k 10 200 python tools/ab_ops.py $op 8 base base%HYGRID_DOWN=0 >> $OUT/ab_ops.txt 2>&1 || exit 1
+done
+timeout -k 10 200 python tools/ab_ops.py rt 8 v0 rt12 rt18 rt24 >> $OUT/ab_ops.txt 2>&1 || exit 1
+cat $OUT/ab_ops.txt
+timeout -k 10 300 python tools/ab_fused.py 8 v0 v05 dmans dmans5 dmans6 > $OUT/ab_fused.txt 2>&1 || exit 1
+cat $OUT/ab_fused.txt
