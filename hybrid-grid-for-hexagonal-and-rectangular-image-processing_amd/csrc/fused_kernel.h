@@ -366,8 +366,10 @@ void k_fused(const Tin* __restrict__ x,
     // to a second __shared__ object make hipcc wait vmcnt(0) for every LDS-DMA in flight.
     // P: 1-KiB pieces per plane row of the group (GW windows of FU_OWN columns + halo)
     constexpr int DP = (GW * FU_OWN + 16 + 511) / 512;
-    constexpr bool DMA = FU_DMA && MD == 0 && sizeof(Tin) == 2 && GW >= C * DP;
-    constexpr bool DST = DMA && FU_DMA_ST && sizeof(Tout) == 2 && GW >= O * DP;
+    // (MD 0 and the pyramid levels MD 3 / 4 / 5; FU_DMA = 2: the pyramid levels only)
+    constexpr bool DMA = (FU_DMA == 1 ? (MD == 0 || MD >= 3) : FU_DMA == 2 ? MD >= 3 : false) &&
+                         sizeof(Tin) == 2 && GW >= C * DP;
+    constexpr bool DST = DMA && MD == 0 && FU_DMA_ST && sizeof(Tout) == 2 && GW >= O * DP;
     constexpr int DPD = FU_DPD, NSR = DPD + 6;
     static_assert(!(DMA && (FU_STAGE || FU_NOMEM)), "FU_DMA replaces FU_STAGE / FU_NOMEM");
     constexpr int DLUT = GW * FU_LUT * 16, DRING = NSR * C * DP * 1024, DSTGB = DST ? 2 * O * DP * 1024 : 0;
@@ -1074,7 +1076,9 @@ void k_fused(const Tin* __restrict__ x,
                 // it are outstanding: DPD steps of (1 piece + the step's stores) (vmcnt counts
                 // loads, stores and LDS-DMA together, in issue order); then the group's barrier
                 // publishes every piece of the row (and orders the staged row's reads)
-                constexpr int N = DPD * (1 + (DST ? 1 : O));
+                // (the pyramid levels store O samples every second step: DPD even keeps the
+                // count exact, the waits otherwise over-count, which is safe)
+                constexpr int N = PYR ? DPD + (DPD / 2) * O : DPD * (1 + (DST ? 1 : O));
                 static_assert(N < 64, "vmcnt");
                 // + lgkmcnt(0): this wave's staged row (LDS writes of the previous step) is in
                 // LDS before the barrier lets the storing waves read it

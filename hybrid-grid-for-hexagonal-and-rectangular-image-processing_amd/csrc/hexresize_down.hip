@@ -9,18 +9,21 @@
 // order alpha*p1 + beta*p2 + gamma*p3 (:354) and 0 for a vertex outside the raster (the
 // reference's masked gather, :336-346), NaN / Inf included.
 //
-// Work unit = (window of nout output columns, band of HD_RB output rows, chunk of planes),
-// one wave each, independent of the other waves of its workgroup:
-//   * lane l owns output columns b = window * nout + K * l + k (k < K); the window's input
-//     columns xb .. xb + 127 (xb from the lattice, host-checked to hold every vertex of the
-//     window: tsk_lattice_ok) are one dword (two 16-bit samples) per lane;
+// Work unit = (window of nout output columns, band of RB output rows, chunk of planes), one
+// wave each, independent of the other waves of its workgroup:
+//   * lane l owns K consecutive output columns b = window * nout + K * l + k; the window's input
+//     columns xb .. xb + WC - 1 (WC = 32 * DB: one DB-byte piece of 16-bit samples per lane; xb
+//     from the lattice, host-checked to hold every vertex of the window: tsk_lattice_ok);
 //   * the band's triangle records are computed once (fp64, per lane, row and column) and kept
 //     in registers for every plane of the chunk: 3 weights + one packed word of vertex
 //     columns / rows / validity;
 //   * per (plane, output row) the two input rows i_n, i_n + 1 arrive in a per-wave LDS ring by
-//     LDS-DMA (buffer_load_dword ... lds, one 256-B row piece per instruction) HD_PDP planes
-//     ahead, so the loads hold no VGPRs; each lane gathers its vertices with ds_read_u16 and
-//     stores its K output samples.
+//     LDS-DMA (buffer_load_dword[x4] ... lds: one 256-B or 1-KiB row piece per instruction) PDP
+//     planes ahead, so the loads hold no VGPRs; each lane gathers its vertices with
+//     ds_read_u16 and stores its K output samples as one 4-16 B piece.
+// Downsampling (ratio >= 0.75 input columns per output column) uses DB = 16 (512-column
+// windows: ~2x hexresize takes 252 output columns per wave, 4 per lane); upsampling DB = 4
+// (128-column windows: 2x up takes 244 output columns per wave, 4 per lane).
 // Waves stride over the units (a grid sized to the resident waves), so a launch has no
 // partial last round.
 #include <algorithm>
@@ -43,9 +46,12 @@ __device__ __forceinline__ void fu_static_for(F&& f) {
 }
 
 constexpr int HD_THREADS = 256;
-constexpr int HD_RB = 4;          // output rows per unit
-constexpr int HD_PDP = 2;         // planes whose rows are in flight ahead (2 x 4 items)
-constexpr int HD_NP = HD_PDP + 1; // ring planes (4 rows x 2 input rows x 64 dwords each)
+constexpr int HD_RING = 8192;     // LDS ring bytes per wave
+
+// (DB: bytes of an input-row piece per lane) -> window columns, rows per unit, planes ahead
+template <int DB> struct TsCfg;
+template <> struct TsCfg<4> { static constexpr int WC = 128, RB = 2, PDP = 2; };
+template <> struct TsCfg<16> { static constexpr int WC = 512, RB = 2, PDP = 1; };
 
 struct HexDownGeom {
     Geom g;                       // make_tri(h, w, h1, w1, margin)
@@ -57,39 +63,41 @@ struct HexDownGeom {
     double qmin;                  // min over output rows of 0.5 i_(a) - s1(a) (window origin)
 };
 
-// packed vertex record of one (row, lane, column): bits 0-7 / 8-15 / 16-23 = window-relative
-// input column of p1 / p2 / p3, bit 24 = p2 in row i_n + 1 (the triangle flag), bits 25-27 = vk
+// packed vertex record of one (row, lane, column): bits 0-8 / 9-17 / 18-26 = window-relative
+// input column of p1 / p2 / p3, bit 27 = p2 in row i_n + 1 (the triangle flag), bits 28-30 = vk
 __device__ __forceinline__ unsigned hd_pack(int o1, int o2, int o3, int flag, int vk) {
-    return (unsigned)o1 | ((unsigned)o2 << 8) | ((unsigned)o3 << 16) | ((unsigned)flag << 24) |
-           ((unsigned)vk << 25);
+    return (unsigned)o1 | ((unsigned)o2 << 9) | ((unsigned)o3 << 18) | ((unsigned)flag << 27) |
+           ((unsigned)vk << 28);
 }
 
 // First input column of window `win`: the lowest vertex column of its outputs (c0 - 1, with
-// c0 = floor(q(a) + f(b)) >= floor(qmin + f(b0))) rounded down to even.  The host check
-// (tsk_lattice_ok) evaluates the same expression.
-__host__ __device__ inline int tsk_window_x0(const Geom& g, double qmin, int b0) {
+// c0 = floor(q(a) + f(b)) >= floor(qmin + f(b0))) rounded down to a multiple of al (the
+// columns of one lane's row piece, so a piece clamped at the left edge holds only columns
+// outside the raster).  The host check (tsk_lattice_ok) evaluates the same expression.
+__host__ __device__ inline int tsk_window_x0(const Geom& g, double qmin, int b0, int al) {
     const double cw = ((double)g.w - 0.5) * 0.5;
     const double f = axis_at(g.ys, b0) + cw;
     const int lo = (int)floor(qmin + f - 1e-6) - 1;
-    return lo >= 0 ? (lo & ~1) : -((-lo + 1) & ~1);
+    return lo >= 0 ? lo - lo % al : -(((-lo) + al - 1) / al * al);
 }
 
-template <typename Tin, typename Tout, int K>
-__global__ __launch_bounds__(HD_THREADS) void k_hexresize_down(const Tin* __restrict__ x,
+template <typename Tin, typename Tout, int K, int DB>
+__global__ __launch_bounds__(HD_THREADS, 4) void k_hexresize_down(const Tin* __restrict__ x,
                                                                Tout* __restrict__ y,
                                                                HexDownGeom D) {
-    static_assert(sizeof(Tin) == 2, "16-bit inputs: one dword = two samples per lane");
-    __shared__ unsigned ring_all[HD_THREADS / 64][HD_NP * 2 * HD_RB][64];
+    static_assert(sizeof(Tin) == 2, "16-bit inputs");
+    constexpr int WC = TsCfg<DB>::WC, RB = TsCfg<DB>::RB, PDP = TsCfg<DB>::PDP, NP = PDP + 1;
+    constexpr int ROWB = WC * 2;                              // ring bytes of one input row
+    static_assert(NP * RB * 2 * ROWB <= HD_RING, "ring");
+    __shared__ __attribute__((aligned(16))) unsigned char ring_all[HD_THREADS / 64][HD_RING];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    unsigned* const ring = &ring_all[wslot][0][0];
+    unsigned char* const ring = ring_all[wslot];
     const int64_t nwaves = (int64_t)gridDim.x * (HD_THREADS / 64);
     const int64_t wid = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (HD_THREADS / 64) + wslot;
     const unsigned rowb = (unsigned)D.w * 2u, planeb = (unsigned)D.h * rowb;
     const unsigned oplane = (unsigned)D.h1 * (unsigned)D.w1 * (unsigned)sizeof(Tout);
     const unsigned orow = (unsigned)D.w1 * (unsigned)sizeof(Tout);
-    // a piece standing in for a loop step's store in the prologue: dropped (no records)
-    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, 0, 0x00020000);
 
     for (int64_t u = wid; u < D.units; u += nwaves) {        // uniform per wave
         const int win = (int)(u % D.nwin);
@@ -98,9 +106,9 @@ __global__ __launch_bounds__(HD_THREADS) void k_hexresize_down(const Tin* __rest
         const int chunk = (int)(r_ / D.nband);
         const int64_t p0 = (int64_t)chunk * D.pc;
         const int np = (int)std::min<int64_t>(D.pc, D.planes - p0);
-        const int a0 = band * HD_RB, nr = min(HD_RB, D.h1 - a0);
+        const int a0 = band * RB, nr = min(RB, D.h1 - a0);
         const int b0 = win * D.nout;
-        const int xb = __builtin_amdgcn_readfirstlane(tsk_window_x0(D.g, D.qmin, b0));
+        const int xb = __builtin_amdgcn_readfirstlane(tsk_window_x0(D.g, D.qmin, b0, DB / 2));
         // the chunk's planes as one buffer each way (host: < 2^31 bytes); a plane >= np
         // reads past the range (zeros)
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -109,109 +117,142 @@ __global__ __launch_bounds__(HD_THREADS) void k_hexresize_down(const Tin* __rest
             (void*)((char*)y + p0 * (int64_t)oplane), (short)0, (int)(np * oplane), 0x00020000);
 
         // ---- the band's triangle records (fp64, geometry_np.py:276-354 via lattice.h) ----
-        float wt[HD_RB][K][3];
-        unsigned pk[HD_RB][K], yo[HD_RB];
-        int r0[HD_RB];
+        float wt[RB][K][3];
+        unsigned pk[RB][K], yo[RB];
+        int r0[RB];
+        const int bl = b0 + K * lane;                        // the lane's first output column
+        const bool lane_live = K * lane < D.nout && bl < D.w1;
+        const bool full = lane_live && bl + K - 1 < D.w1;    // all K columns in the raster
 #pragma unroll
-        for (int k = 0; k < HD_RB; ++k) {
+        for (int k = 0; k < RB; ++k) {
+            // rows past the band's last (k >= nr) repeat its records, so they store the same
+            // values to the same row: every store has in-range lanes (a store whose lanes are
+            // all out of range can retire ahead of older loads and break the counted waits)
             const int a = a0 + min(k, nr - 1);
 #pragma unroll
             for (int kk = 0; kk < K; ++kk) {
-                const int bb = b0 + K * lane + kk;
-                const bool own = K * lane + kk < D.nout && bb < D.w1;
+                const int bb = bl + kk;
+                const bool own = lane_live && bb < D.w1;
                 const TriSample s = tri_sample(D.g, a, own ? bb : b0);
                 if (kk == 0) r0[k] = __builtin_amdgcn_readfirstlane((int)s.i_n);   // i_n: row only
                 const int e = (int)(s.r[2] == s.r[0] ? 0 : (s.c[0] + 1 - s.c[2]));   // s2 - s1
                 const int c0 = (int)s.c[0] - xb;
-                const int o1 = min(max(c0, 0), 127);
-                const int o2 = min(max(s.flag ? c0 - e : c0 + 1, 0), 127);
-                const int o3 = min(max(c0 + 1 - e, 0), 127);
+                const int o1 = min(max(c0, 0), WC - 1);
+                const int o2 = min(max(s.flag ? c0 - e : c0 + 1, 0), WC - 1);
+                const int o3 = min(max(c0 + 1 - e, 0), WC - 1);
                 wt[k][kk][0] = (float)s.alpha;
                 wt[k][kk][1] = (float)s.beta;
                 wt[k][kk][2] = (float)s.gamma;
                 pk[k][kk] = hd_pack(o1, o2, o3, s.flag, s.vk);
             }
-            const int bl = b0 + K * lane;
-            const bool live = K * lane < D.nout && bl < D.w1 && k < nr;
-            yo[k] = live ? (unsigned)(a0 + k) * orow + (unsigned)bl * (unsigned)sizeof(Tout) : 0x80000000u;
+            yo[k] = lane_live ? (unsigned)a * orow + (unsigned)bl * (unsigned)sizeof(Tout) : 0x80000000u;
         }
 
-        // K == 2: both of the lane's columns inside the raster (else the first one alone)
-        const bool pair = b0 + K * lane + 1 < D.w1;
-        // ---- (plane, row) items: LDS-DMA of rows i_n, i_n + 1 of plane pi + HD_PDP -------
-        // (columns left of the raster: the lane's dword is clamped to column 0 and every
+        // ---- (plane, row) items: LDS-DMA of rows i_n, i_n + 1 of plane pi + PDP ----------
+        // (columns left of the raster: the lane's piece is clamped to column 0 and every
         // vertex there is outside the raster, masked by vk)
-        const unsigned voff = (unsigned)max(xb + 2 * lane, 0) * 2u;
-        auto slots = [&](int pi) { return ring + (pi % HD_NP) * (2 * HD_RB * 64); };
+        const unsigned voff = (unsigned)max(xb + (DB / 2) * lane, 0) * 2u;
+        auto slots = [&](int pi) { return ring + (pi % NP) * (2 * RB * ROWB); };
         auto dma = [&](int pi, auto Kc) {
             constexpr int k = decltype(Kc)::value;
-            unsigned* const sl = slots(pi) + 2 * k * 64;
+            unsigned char* const sl = slots(pi) + 2 * k * ROWB;
             const unsigned po = pi < np ? (unsigned)pi * planeb : (unsigned)np * planeb;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const unsigned so = po + (unsigned)(r0[k] + q) * rowb;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    xr, (__attribute__((address_space(3))) void*)(sl + q * 64), 4, voff, so, 0, 0);
+                auto* const ld = (__attribute__((address_space(3))) void*)(sl + q * ROWB);
+                if constexpr (DB == 16)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, ld, 16, voff, so, 0, 0);
+                else
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, ld, 4, voff, so, 0, 0);
             }
         };
-        // prologue: planes 0 .. HD_PDP - 1, each item followed by a dropped store standing in
-        // for the store a loop step issues, so the wait count below is the same every step
-        for (int pi = 0; pi < HD_PDP; ++pi) {
-            fu_static_for<HD_RB>([&](auto Kc) {
-                dma(pi, Kc);
-                __builtin_amdgcn_raw_buffer_store_b32(0u, none, 0x80000000u, 0, 0);
-            });
-        }
+        // prologue: the items of planes 0 .. PDP - 1
+        for (int pi = 0; pi < PDP; ++pi) fu_static_for<RB>([&](auto Kc) { dma(pi, Kc); });
         for (int pi = 0; pi < np; ++pi) {
             const unsigned short* const base = reinterpret_cast<const unsigned short*>(slots(pi));
             const unsigned yp = (unsigned)pi * oplane;
-            fu_static_for<HD_RB>([&](auto Kc) {
+            fu_static_for<RB>([&](auto Kc) {
                 constexpr int k = decltype(Kc)::value;
-                dma(pi + HD_PDP, Kc);
-                // item (pi, k)'s two pieces are done once at most the operations issued after
-                // them are outstanding: 4 * HD_PDP steps of (2 pieces + 1 store) (vmcnt counts
-                // loads, stores and LDS-DMA together, in issue order)
-                constexpr int N = 3 * HD_RB * HD_PDP;
-                static_assert(N < 64, "vmcnt");
-                __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf) | ((N >> 4) << 14));
+                dma(pi + PDP, Kc);
+                // item t = (pi, k)'s two pieces are done once at most the operations issued
+                // after them are outstanding (vmcnt counts loads, stores and LDS-DMA together,
+                // in issue order): the pieces of the RB * PDP items after it and the stores of
+                // the loop steps since -- 2 RB PDP + min(t, RB PDP)
+                constexpr int NPC = 2 * RB * PDP, NST = RB * PDP;
+                static_assert(NPC + NST < 64, "vmcnt");
+                auto wait = [](auto Nc) {
+                    constexpr int N = decltype(Nc)::value;
+                    __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf) | ((N >> 4) << 14));
+                };
+                if (pi >= PDP) {
+                    wait(std::integral_constant<int, NPC + NST>{});
+                } else {
+                    fu_static_for<PDP>([&](auto Pc) {
+                        constexpr int P = decltype(Pc)::value;
+                        if (pi == P) wait(std::integral_constant<int, NPC + P * RB + k>{});
+                    });
+                }
                 asm volatile("" ::: "memory");                    // LDS reads after the wait
-                const unsigned short* const s0 = base + 2 * k * 128;
-                const unsigned short* const s1 = s0 + 128;
+                const unsigned short* const s0 = base + 2 * k * WC;
+                const unsigned short* const s1 = s0 + WC;
                 float v[K];
 #pragma unroll
                 for (int kk = 0; kk < K; ++kk) {
                     const unsigned q = pk[k][kk];
-                    const unsigned short h1 = s0[q & 255];
-                    const unsigned short h2 = ((q >> 24) & 1) ? s1[(q >> 8) & 255] : s0[(q >> 8) & 255];
-                    const unsigned short h3 = s1[(q >> 16) & 255];
-                    const float v0 = ((q >> 25) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h1)) : 0.f;
-                    const float v1 = ((q >> 26) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h2)) : 0.f;
-                    const float v2 = ((q >> 27) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h3)) : 0.f;
+                    const unsigned short h1 = s0[q & 511];
+                    const unsigned short h2 = ((q >> 27) & 1) ? s1[(q >> 9) & 511] : s0[(q >> 9) & 511];
+                    const unsigned short h3 = s1[(q >> 18) & 511];
+                    const float v0 = ((q >> 28) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h1)) : 0.f;
+                    const float v1 = ((q >> 29) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h2)) : 0.f;
+                    const float v2 = ((q >> 30) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h3)) : 0.f;
                     v[kk] = wt[k][kk][0] * v0 + wt[k][kk][1] * v1 + wt[k][kk][2] * v2;   // :354
                 }
-                if constexpr (K == 1 && sizeof(Tout) == 2) {
-                    __builtin_amdgcn_raw_buffer_store_b16(
-                        __builtin_bit_cast(unsigned short, from_acc<Tout>(v[0])), yr, yo[k], yp, 0);
-                } else if constexpr (K == 1) {
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), yr, yo[k], yp, 0);
-                } else if (pair) {                          // K == 2: the lane's column pair
+                if (full) {                                      // the lane's K columns at once
                     if constexpr (sizeof(Tout) == 2) {
-                        typedef Tout t2v __attribute__((ext_vector_type(2)));
-                        __builtin_amdgcn_raw_buffer_store_b32(
-                            __builtin_bit_cast(unsigned, t2v{from_acc<Tout>(v[0]), from_acc<Tout>(v[1])}),
-                            yr, yo[k], yp, 0);
+                        unsigned pw[K / 2 > 0 ? K / 2 : 1];
+#pragma unroll
+                        for (int i = 0; i < K / 2; ++i) {
+                            typedef Tout t2v __attribute__((ext_vector_type(2)));
+                            pw[i] = __builtin_bit_cast(unsigned, t2v{from_acc<Tout>(v[2 * i]), from_acc<Tout>(v[2 * i + 1])});
+                        }
+                        if constexpr (K == 1)
+                            __builtin_amdgcn_raw_buffer_store_b16(
+                                __builtin_bit_cast(unsigned short, from_acc<Tout>(v[0])), yr, yo[k], yp, 0);
+                        else if constexpr (K == 2)
+                            __builtin_amdgcn_raw_buffer_store_b32(pw[0], yr, yo[k], yp, 0);
+                        else {
+                            typedef unsigned u2v __attribute__((ext_vector_type(2)));
+                            __builtin_amdgcn_raw_buffer_store_b64(u2v{pw[0], pw[1]}, yr, yo[k], yp, 0);
+                        }
                     } else {
-                        typedef unsigned u2v __attribute__((ext_vector_type(2)));
-                        __builtin_amdgcn_raw_buffer_store_b64(
-                            u2v{__builtin_bit_cast(unsigned, v[0]), __builtin_bit_cast(unsigned, v[1])},
-                            yr, yo[k], yp, 0);
+                        if constexpr (K == 1) {
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), yr, yo[k], yp, 0);
+                        } else if constexpr (K == 2) {
+                            typedef unsigned u2v __attribute__((ext_vector_type(2)));
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                u2v{__builtin_bit_cast(unsigned, v[0]), __builtin_bit_cast(unsigned, v[1])},
+                                yr, yo[k], yp, 0);
+                        } else {
+                            typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                            __builtin_amdgcn_raw_buffer_store_b128(
+                                u4v{__builtin_bit_cast(unsigned, v[0]), __builtin_bit_cast(unsigned, v[1]),
+                                    __builtin_bit_cast(unsigned, v[2]), __builtin_bit_cast(unsigned, v[3])},
+                                yr, yo[k], yp, 0);
+                        }
                     }
-                } else {   // an odd width's last column alone (a second store: waits over-count)
-                    if constexpr (sizeof(Tout) == 2)
-                        __builtin_amdgcn_raw_buffer_store_b16(
-                            __builtin_bit_cast(unsigned short, from_acc<Tout>(v[0])), yr, yo[k], yp, 0);
-                    else
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), yr, yo[k], yp, 0);
+                } else {   // the raster's last columns: one store per column (the extra stores
+                           // only over-count the waits above)
+#pragma unroll
+                    for (int kk = 0; kk < K; ++kk) {
+                        const unsigned o = (lane_live && bl + kk < D.w1) ? yo[k] + kk * (unsigned)sizeof(Tout)
+                                                                         : 0x80000000u;
+                        if constexpr (sizeof(Tout) == 2)
+                            __builtin_amdgcn_raw_buffer_store_b16(
+                                __builtin_bit_cast(unsigned short, from_acc<Tout>(v[kk])), yr, o, yp, 0);
+                        else
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[kk]), yr, o, yp, 0);
+                    }
                 }
             });
         }
@@ -220,7 +261,7 @@ __global__ __launch_bounds__(HD_THREADS) void k_hexresize_down(const Tin* __rest
     }
 }
 
-// Does every window of nout output columns keep its triangle vertices inside its 128 input
+// Does every window of nout output columns keep its triangle vertices inside its WC input
 // columns?  With s1(a) = trunc((i_n + 1) / 2) (geometry_np.py:289) and j_ = 0.5 i_ + y_(b) +
 // (w - 0.5) / 2 (:277), c0 = j_n - s1 = floor(q(a) + f(b)) for q(a) = 0.5 i_(a) - s1(a) and
 // f(b) = y_(b) + (w - 0.5) / 2 (f increasing), and every vertex lies in c0 - 1 .. c0 + 1; so a
@@ -228,56 +269,61 @@ __global__ __launch_bounds__(HD_THREADS) void k_hexresize_down(const Tin* __rest
 // the window origin the kernel computes (tsk_window_x0), with a margin for the fp64 rounding
 // of j_ and one column for a j_ truncated towards 0 at the left edge.  O(h1 + w1 / nout).
 // The rows are free: each (plane, output row) loads its own rows i_n, i_n + 1.
-static bool tsk_lattice_ok(const Geom& g, int nout, double* qmin_out) {
-    double qmin = 1e300, qmax = -1e300;
-    const double ch = (double)(g.h - 1) * 0.5, cw = ((double)g.w - 0.5) * 0.5;
+static bool tsk_rows_ok(const Geom& g, double* qmin, double* qmax) {
+    *qmin = 1e300;
+    *qmax = -1e300;
+    const double ch = (double)(g.h - 1) * 0.5;
     for (int64_t a = 0; a < g.h1; ++a) {
         const double i_ = axis_at(g.xs, a) + ch;
         const int64_t in = (int64_t)i_;
         if (in < 0 || in >= g.h) return false;
         const int64_t s1 = (int64_t)((double)(in + 1) / 2.0);
         const double q = 0.5 * i_ - (double)s1;
-        qmin = std::min(qmin, q);
-        qmax = std::max(qmax, q);
+        *qmin = std::min(*qmin, q);
+        *qmax = std::max(*qmax, q);
     }
+    return true;
+}
+
+static bool tsk_lattice_ok(const Geom& g, int nout, int wc, double qmin, double qmax) {
+    const double cw = ((double)g.w - 0.5) * 0.5;
     const int64_t nwin = (g.w1 + nout - 1) / nout;
     for (int64_t wi = 0; wi < nwin; ++wi) {
         const int b0 = (int)(wi * nout);
         const int b1 = (int)std::min<int64_t>(b0 + nout, g.w1) - 1;
-        const int x0 = tsk_window_x0(g, qmin, b0);
+        const int x0 = tsk_window_x0(g, qmin, b0, wc / 64);
         const int hi = (int)floor(qmax + axis_at(g.ys, b1) + cw + 1e-6) + 2;
-        if (hi - x0 > 127) return false;
+        if (hi - x0 > wc - 1) return false;
     }
-    *qmin_out = qmin;
     return true;
 }
 
-template <typename Tin, typename Tout, int K>
+template <typename Tin, typename Tout, int K, int DB>
 static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st) {
     // resident waves: 256 CUs x 4 SIMDs x 4 waves; units split into plane chunks until
     // there are >= 4 units per resident wave (the records are then recomputed per chunk)
     constexpr int64_t RESIDENT = 256 * 4 * 4;
+    constexpr int PDP = TsCfg<DB>::PDP;
     const int64_t tiles = (int64_t)D.nwin * D.nband;
     int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, (4 * RESIDENT + tiles - 1) / tiles));
     // a chunk's planes are one buffer each way: 32-bit offsets, including the planes past
     // the chunk the prefetch addresses (out of range: zeros)
     const int64_t plane_bytes = std::max<int64_t>((int64_t)D.h * D.w * 2, (int64_t)D.h1 * D.w1 * 4);
-    const int64_t max_pc = std::max<int64_t>(1, (((int64_t)1 << 31) - 1) / plane_bytes - HD_PDP - 1);
+    const int64_t max_pc = std::max<int64_t>(1, (((int64_t)1 << 31) - 1) / plane_bytes - PDP - 1);
     nchunk = std::max<int64_t>(nchunk, (D.planes + max_pc - 1) / max_pc);
     D.pc = (int)((D.planes + nchunk - 1) / nchunk);
     D.nchunk = (int)((D.planes + D.pc - 1) / D.pc);
     D.units = tiles * D.nchunk;
     const int64_t waves = std::min<int64_t>(D.units, RESIDENT);
     const unsigned blocks = (unsigned)((waves + 3) / 4);
-    hipLaunchKernelGGL((k_hexresize_down<Tin, Tout, K>), dim3(blocks), dim3(HD_THREADS), 0, st,
+    hipLaunchKernelGGL((k_hexresize_down<Tin, Tout, K, DB>), dim3(blocks), dim3(HD_THREADS), 0, st,
                        (const Tin*)src, (Tout*)dst, D);
     return launch_status();
 }
 
 // A triangle-blend resample (op: HG_OP_HEXRESIZE or HG_OP_HEX_TO_RECT, linear) on the
 // streaming kernel, or HG_EUNSUP (the caller runs k_resample_lds).  dry: check only (HG_OK if
-// the kernel would run).  Output columns per lane: 1 when the lattice steps at least ~one
-// input column per output column (downsampling), else 2.
+// the kernel would run).
 int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h,
                   int64_t w, int64_t h1, int64_t w1, hipStream_t st, bool dry) {
     if (env_is("HYGRID_DOWN", "0")) return HG_EUNSUP;   // A/B switch: general kernels only
@@ -286,30 +332,39 @@ int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t 
     if (ddt != HG_F16 && ddt != HG_BF16 && ddt != HG_F32) return HG_EUNSUP;
     if (planes < 1 || h < 2 || w < 2 || h1 < 1 || w1 < 1) return HG_EUNSUP;
     // LDS-DMA moves whole dwords from dword-aligned addresses: every input row must start on
-    // one (even width, 4-B aligned base)
+    // one (even width, 4-B aligned base); 16-B pieces want 16-B aligned rows
     if ((w & 1) || (reinterpret_cast<uintptr_t>(src) & 3)) return HG_EUNSUP;
+    const bool a16 = (w % 8) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0;
     // one plane (+ the prefetch's out-of-range planes) within 32-bit buffer offsets
-    if ((h * w * 2) * (HD_PDP + 2) >= ((int64_t)1 << 31) ||
-        (h1 * w1 * 4) * (HD_PDP + 2) >= ((int64_t)1 << 31))
+    if ((h * w * 2) * 4 >= ((int64_t)1 << 31) || (h1 * w1 * 4) * 4 >= ((int64_t)1 << 31))
         return HG_EUNSUP;
     const Geom g = make_tri(h, w, h1, w1, op == HG_OP_HEXRESIZE ? 0.5 : 0.75);
-    // columns per output column; two output columns per lane when below one
+    // input columns per output column: 512-column windows (16-B pieces) when downsampling,
+    // 128-column windows (4-B pieces) when upsampling or the rows are not 16-B aligned; lane
+    // l owns output columns K l .. K l + K - 1 of its window (K = 4, or 1 for narrow windows)
     const double ratio = w1 > 1 ? (double)(w - 1) / (double)(w1 - 1) : 1.0;
-    const int K = ratio < 0.75 ? 2 : 1;
+    const int DB = (ratio >= 0.75 && a16) ? 16 : 4, wc = 32 * DB;
     HexDownGeom D = {};
-    int nout = std::min(64 * K, (int)std::floor(122.0 / std::max(ratio, 1e-3)));
-    for (; nout >= 16; nout -= 2)
-        if (tsk_lattice_ok(g, nout, &D.qmin)) break;
-    if (nout < 16) return HG_EUNSUP;
+    double qmax;
+    if (!tsk_rows_ok(g, &D.qmin, &qmax)) return HG_EUNSUP;
+    int nout = std::min(256, (int)std::floor((wc - 6) / std::max(ratio, 1e-3)));
+    for (; nout >= 32; --nout) {
+        if (nout > 64 && (nout & 3)) continue;       // whole lanes of K = 4
+        if (tsk_lattice_ok(g, nout, wc, D.qmin, qmax)) break;
+    }
+    if (nout < 32) return HG_EUNSUP;                  // > ~15x downsampling: the general kernel
+    const int K = nout > 64 ? 4 : 1;
     D.g = g;
     D.planes = planes;
     D.h = (int)h; D.w = (int)w; D.h1 = (int)h1; D.w1 = (int)w1;
     D.nout = nout;
     D.nwin = (int)((w1 + nout - 1) / nout);
-    D.nband = (int)((h1 + HD_RB - 1) / HD_RB);
+    D.nband = (int)((h1 + (DB == 16 ? TsCfg<16>::RB : TsCfg<4>::RB) - 1) /
+                    (DB == 16 ? TsCfg<16>::RB : TsCfg<4>::RB));
     if (dry) return HG_OK;
 #define HG_TSK(TI, TO)                                                                         \
-    return K == 2 ? hd_launch<TI, TO, 2>(src, dst, D, st) : hd_launch<TI, TO, 1>(src, dst, D, st);
+    if (DB == 4) return K == 4 ? hd_launch<TI, TO, 4, 4>(src, dst, D, st) : hd_launch<TI, TO, 1, 4>(src, dst, D, st); \
+    return K == 4 ? hd_launch<TI, TO, 4, 16>(src, dst, D, st) : hd_launch<TI, TO, 1, 16>(src, dst, D, st);
     if (sdt == HG_BF16) {
         if (ddt == HG_BF16) { HG_TSK(__bf16, __bf16) }
         if (ddt == HG_F16) { HG_TSK(__bf16, _Float16) }

@@ -58,11 +58,11 @@ def main():
     else:
         B, C, H, W, t = 8, 3, 4320, 7680, torch.float16
     x = torch.rand((B, C, H, W), generator=g, device=dev, dtype=t)
+    taps = (torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32, device=dev) / 12).repeat(C)
     if op.startswith("pyr") or op.startswith("hr"):
         y = torch.empty((B, C, H // 2, W // 2), device=dev, dtype=t)
     elif op == "up":
         y = torch.empty((B, C, 2 * H, 2 * W), device=dev, dtype=t)
-        taps = (torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32, device=dev) / 12).repeat(C)
     else:
         y = torch.empty_like(x)
     kc = C if op == "wide" else 3

@@ -61,7 +61,7 @@ def main():
         labels = {}
         insts = []      # (index, text)
         for ln in body:
-            s = ln.strip()
+            s = ln.split(";")[0].strip()
             if not s or s.startswith((";", ".")) and not s.startswith(".LBB"):
                 continue
             if s.startswith(".LBB") and s.endswith(":"):

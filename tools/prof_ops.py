@@ -1,0 +1,52 @@
+"""Profiling driver for the secondary lines: runs one call a few times so rocprofv3 (kernel
+trace / PMC passes) can attribute its kernel.
+
+usage: python tools/prof_ops.py OP [iters]
+  rt   config 2: fused rect -> hex -> rect round trip, 1080p fp32 b32 (k_fused MD 2)
+  pyr0 config 5 level 0 from the rect image, 8K fp16 b8 (k_fused MD 3)
+  pyr1 config 5 level 1 (4K -> 2K from a hex image)
+  hr0  hexresize 8K -> 4K fp16 b8 (the pyramid chain's level-0 hexresize)
+  up   hex (1080, 1920) -> rect (2160, 3840) bf16 b32
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "hybrid-grid-for-hexagonal-and-rectangular-image-processing_amd")]
+
+import torch  # noqa: E402
+
+from HyGrid import ops  # noqa: E402
+from HyGrid.pipeline import rect_hex_rect  # noqa: E402
+
+
+def main():
+    op = sys.argv[1]
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    dev = torch.device("cuda:0")
+    if op == "rt":
+        x = torch.rand((32, 3, 1080, 1920), device=dev)
+        fn = lambda: rect_hex_rect(x)  # noqa: E731
+    elif op in ("pyr0", "pyr1"):
+        shape = (8, 3, 4320, 7680) if op == "pyr0" else (8, 3, 2160, 3840)
+        x = torch.rand(shape, device=dev, dtype=torch.float16)
+        taps = (torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32, device=dev) / 12).repeat(3, 1)
+        H, W = shape[-2:]
+        fn = lambda: ops.hex_pyramid_level(x, taps, None, (H // 2, W // 2), 0,  # noqa: E731
+                                           from_rect=(op == "pyr0"), out_dtype=torch.float16)
+    elif op == "hr0":
+        x = torch.rand((8, 3, 4320, 7680), device=dev, dtype=torch.float16)
+        fn = lambda: ops.hexresize(x, (2160, 3840), out_dtype=torch.float16)  # noqa: E731
+    elif op == "up":
+        x = torch.rand((32, 3, 1080, 1920), device=dev, dtype=torch.bfloat16)
+        fn = lambda: ops.hex_to_rect(x, (2160, 3840))  # noqa: E731
+    else:
+        raise SystemExit(f"unknown op {op}")
+    with torch.no_grad():
+        for _ in range(iters):
+            fn()
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

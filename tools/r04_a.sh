@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 GPU session A: new parity tests (streaming triangle kernel, pyramid kernel
-# selection / overflow, bf16-exact MFMA weights, cross-dtype r2h down), then A/Bs.
+# selection / overflow, bf16-exact MFMA weights, cross-dtype r2h down), then A/Bs and the
+# secondary lines' SQ / traffic counters.
 set -o pipefail
 OUT=gpurun_out/r04a; mkdir -p $OUT
 export TMPDIR=/tmp
@@ -13,6 +14,13 @@ for op in hr0 hr1 hr2 up; do
   timeout -k 10 200 python tools/ab_ops.py $op 8 base base%HYGRID_DOWN=0 >> $OUT/ab_ops.txt 2>&1 || exit 1
 done
 timeout -k 10 200 python tools/ab_ops.py rt 8 v0 rt12 rt18 rt24 >> $OUT/ab_ops.txt 2>&1 || exit 1
+for op in pyrfr pyr1 pyr2; do
+  timeout -k 10 200 python tools/ab_ops.py $op 8 p0 pdma pdma2 >> $OUT/ab_ops.txt 2>&1 || exit 1
+done
 cat $OUT/ab_ops.txt
 timeout -k 10 300 python tools/ab_fused.py 8 v0 v05 dmans dmans5 dmans6 > $OUT/ab_fused.txt 2>&1 || exit 1
 cat $OUT/ab_fused.txt
+for op in rt pyr0; do
+  bash tools/pmc_kernel.sh r04a/pmc_$op k_fused -- python3 tools/prof_ops.py $op 3 > $OUT/pmc_$op.log 2>&1 || { tail -5 $OUT/pmc_$op.log; exit 1; }
+done
+tail -30 $OUT/pmc_rt.log $OUT/pmc_pyr0.log
