@@ -45,13 +45,39 @@ __device__ __forceinline__ void fu_static_for(F&& f) {
     }
 }
 
+// tuning knobs (A/B variants: tools/build_ovariant.sh)
+#ifndef HD_RB16
+#define HD_RB16 2           // 16-B pieces: output rows per unit
+#endif
+#ifndef HD_PDP16
+#define HD_PDP16 1          // 16-B pieces: planes in flight ahead of the one blended
+#endif
+#ifndef HD_RB4
+#define HD_RB4 2
+#endif
+#ifndef HD_PDP4
+#define HD_PDP4 2
+#endif
+#ifndef HD_P16
+#define HD_P16 1            // 16-B pieces: adjacent output columns per lane and store
+#endif
+#ifndef HD_P4
+#define HD_P4 2
+#endif
+#ifndef HD_WPE
+#define HD_WPE 4            // waves per SIMD asked of the register allocator
+#endif
+#ifndef HD_RING
+#define HD_RING 8576        // LDS ring bytes per wave
+#endif
 constexpr int HD_THREADS = 256;
-constexpr int HD_RING = 8192;     // LDS ring bytes per wave
 
-// (DB: bytes of an input-row piece per lane) -> window columns, rows per unit, planes ahead
+// (DB: bytes of an input-row piece per lane) -> window columns (64 lanes x DB bytes + one
+// 32-B piece of 8 lanes), rows per unit, planes ahead; a ring row holds the window's WC
+// samples and a 16-B zero slot (the vertices outside the raster read it)
 template <int DB> struct TsCfg;
-template <> struct TsCfg<4> { static constexpr int WC = 128, RB = 2, PDP = 2; };
-template <> struct TsCfg<16> { static constexpr int WC = 512, RB = 2, PDP = 1; };
+template <> struct TsCfg<4> { static constexpr int WC = 144, RB = HD_RB4, PDP = HD_PDP4; };
+template <> struct TsCfg<16> { static constexpr int WC = 528, RB = HD_RB16, PDP = HD_PDP16; };
 
 struct HexDownGeom {
     Geom g;                       // make_tri(h, w, h1, w1, margin)
@@ -63,11 +89,12 @@ struct HexDownGeom {
     double qmin;                  // min over output rows of 0.5 i_(a) - s1(a) (window origin)
 };
 
-// packed vertex record of one (row, lane, column): bits 0-8 / 9-17 / 18-26 = window-relative
-// input column of p1 / p2 / p3, bit 27 = p2 in row i_n + 1 (the triangle flag), bits 28-30 = vk
-__device__ __forceinline__ unsigned hd_pack(int o1, int o2, int o3, int flag, int vk) {
-    return (unsigned)o1 | ((unsigned)o2 << 9) | ((unsigned)o3 << 18) | ((unsigned)flag << 27) |
-           ((unsigned)vk << 28);
+// packed vertex record of one (row, lane, column): the ring index (16-bit samples) of p1 in
+// row i_n (bits 0-9), of p2 from row i_n's start (bits 10-20: + the row pitch when the
+// triangle flag puts it in row i_n + 1) and of p3 in row i_n + 1 (bits 21-30); a vertex
+// outside the raster indexes its row's zero slot (the reference's masked gather reads 0)
+__device__ __forceinline__ unsigned hd_pack(int o1, int o2, int o3) {
+    return (unsigned)o1 | ((unsigned)o2 << 10) | ((unsigned)o3 << 21);
 }
 
 // First input column of window `win`: the lowest vertex column of its outputs (c0 - 1, with
@@ -81,18 +108,23 @@ __host__ __device__ inline int tsk_window_x0(const Geom& g, double qmin, int b0,
     return lo >= 0 ? lo - lo % al : -(((-lo) + al - 1) / al * al);
 }
 
-template <typename Tin, typename Tout, int K, int DB>
-__global__ __launch_bounds__(HD_THREADS, 4) void k_hexresize_down(const Tin* __restrict__ x,
+template <typename Tin, typename Tout, int K, int DB, int P>
+__global__ __launch_bounds__(HD_THREADS, HD_WPE) void k_hexresize_down(const Tin* __restrict__ x,
                                                                Tout* __restrict__ y,
                                                                HexDownGeom D) {
     static_assert(sizeof(Tin) == 2, "16-bit inputs");
     constexpr int WC = TsCfg<DB>::WC, RB = TsCfg<DB>::RB, PDP = TsCfg<DB>::PDP, NP = PDP + 1;
-    constexpr int ROWB = WC * 2;                              // ring bytes of one input row
-    static_assert(NP * RB * 2 * ROWB <= HD_RING, "ring");
+    constexpr int ROWB = WC * 2 + 16;                         // ring bytes of one input row
+    constexpr int RW = ROWB / 2;                              // the same in samples
+    static_assert(NP * RB * 2 * ROWB <= HD_RING && WC < 1024 && 2 * RW < 2048, "ring");
     __shared__ __attribute__((aligned(16))) unsigned char ring_all[HD_THREADS / 64][HD_RING];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     unsigned char* const ring = ring_all[wslot];
+    if (lane < NP * RB * 2) {                                 // the zero slots (never DMA'd)
+        typedef unsigned u4v __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<u4v*>(ring + lane * ROWB + 2 * WC) = u4v{0u, 0u, 0u, 0u};
+    }
     const int64_t nwaves = (int64_t)gridDim.x * (HD_THREADS / 64);
     const int64_t wid = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x) * (HD_THREADS / 64) + wslot;
     const unsigned rowb = (unsigned)D.w * 2u, planeb = (unsigned)D.h * rowb;
@@ -117,12 +149,15 @@ __global__ __launch_bounds__(HD_THREADS, 4) void k_hexresize_down(const Tin* __r
             (void*)((char*)y + p0 * (int64_t)oplane), (short)0, (int)(np * oplane), 0x00020000);
 
         // ---- the band's triangle records (fp64, geometry_np.py:276-354 via lattice.h) ----
+        // lane l owns the columns b0 + P l + 64 P j + p (j < K / P, p < P) of its window: P
+        // adjacent columns per store, the lanes of one store consecutive (so the gathers of
+        // one ds_read hit consecutive LDS dwords, and one store covers 64 P columns)
+        static_assert(K % P == 0, "K");
+        constexpr int NJ = K / P;
         float wt[RB][K][3];
         unsigned pk[RB][K], yo[RB];
         int r0[RB];
-        const int bl = b0 + K * lane;                        // the lane's first output column
-        const bool lane_live = K * lane < D.nout && bl < D.w1;
-        const bool full = lane_live && bl + K - 1 < D.w1;    // all K columns in the raster
+        const int bend = min(b0 + D.nout, D.w1);            // the window's end column
 #pragma unroll
         for (int k = 0; k < RB; ++k) {
             // rows past the band's last (k >= nr) repeat its records, so they store the same
@@ -131,27 +166,40 @@ __global__ __launch_bounds__(HD_THREADS, 4) void k_hexresize_down(const Tin* __r
             const int a = a0 + min(k, nr - 1);
 #pragma unroll
             for (int kk = 0; kk < K; ++kk) {
-                const int bb = bl + kk;
-                const bool own = lane_live && bb < D.w1;
-                const TriSample s = tri_sample(D.g, a, own ? bb : b0);
+                const int bb = b0 + P * lane + 64 * P * (kk / P) + kk % P;
+                const TriSample s = tri_sample(D.g, a, bb < bend ? bb : b0);
                 if (kk == 0) r0[k] = __builtin_amdgcn_readfirstlane((int)s.i_n);   // i_n: row only
-                const int e = (int)(s.r[2] == s.r[0] ? 0 : (s.c[0] + 1 - s.c[2]));   // s2 - s1
-                const int c0 = (int)s.c[0] - xb;
-                const int o1 = min(max(c0, 0), WC - 1);
-                const int o2 = min(max(s.flag ? c0 - e : c0 + 1, 0), WC - 1);
-                const int o3 = min(max(c0 + 1 - e, 0), WC - 1);
+                auto ix = [&](int v) {                           // vertex v's ring index
+                    return (s.vk >> v) & 1 ? min(max((int)s.c[v] - xb, 0), WC - 1) : WC;
+                };
                 wt[k][kk][0] = (float)s.alpha;
                 wt[k][kk][1] = (float)s.beta;
                 wt[k][kk][2] = (float)s.gamma;
-                pk[k][kk] = hd_pack(o1, o2, o3, s.flag, s.vk);
+                pk[k][kk] = hd_pack(ix(0), (s.r[1] != s.r[0] && ((s.vk >> 1) & 1) ? RW : 0) + ix(1), ix(2));
             }
-            yo[k] = lane_live ? (unsigned)a * orow + (unsigned)bl * (unsigned)sizeof(Tout) : 0x80000000u;
+            yo[k] = (unsigned)a * orow;
+        }
+        // per store j: the lane's byte offset in the row when all its P columns are in the
+        // window; else lane 0 (whose column b0 always is, and b0 + 1 for P = 2: host) repeats
+        // store 0, so no store has all its lanes out of range; a lane with only its first
+        // column inside stores that one separately (pc1)
+        unsigned co[NJ];
+        bool pc1[NJ], rep[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int c = b0 + P * lane + 64 * P * j;
+            const bool all = c + P - 1 < bend;
+            rep[j] = !all && lane == 0;
+            co[j] = all ? (unsigned)c * (unsigned)sizeof(Tout)
+                        : lane == 0 ? (unsigned)b0 * (unsigned)sizeof(Tout) : 0x80000000u;
+            pc1[j] = P == 2 && !all && c < bend;
         }
 
         // ---- (plane, row) items: LDS-DMA of rows i_n, i_n + 1 of plane pi + PDP ----------
         // (columns left of the raster: the lane's piece is clamped to column 0 and every
         // vertex there is outside the raster, masked by vk)
         const unsigned voff = (unsigned)max(xb + (DB / 2) * lane, 0) * 2u;
+        const unsigned voff2 = (unsigned)max(xb + 32 * DB + 2 * lane, 0) * 2u;
         auto slots = [&](int pi) { return ring + (pi % NP) * (2 * RB * ROWB); };
         auto dma = [&](int pi, auto Kc) {
             constexpr int k = decltype(Kc)::value;
@@ -165,6 +213,9 @@ __global__ __launch_bounds__(HD_THREADS, 4) void k_hexresize_down(const Tin* __r
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, ld, 16, voff, so, 0, 0);
                 else
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, ld, 4, voff, so, 0, 0);
+                // the window's last 16 columns: one dword each from lanes 0-7
+                auto* const le = (__attribute__((address_space(3))) void*)(sl + q * ROWB + 64 * DB);
+                if (lane < 8) __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, le, 4, voff2, so, 0, 0);
             }
         };
         // prologue: the items of planes 0 .. PDP - 1
@@ -177,9 +228,9 @@ __global__ __launch_bounds__(HD_THREADS, 4) void k_hexresize_down(const Tin* __r
                 dma(pi + PDP, Kc);
                 // item t = (pi, k)'s two pieces are done once at most the operations issued
                 // after them are outstanding (vmcnt counts loads, stores and LDS-DMA together,
-                // in issue order): the pieces of the RB * PDP items after it and the stores of
-                // the loop steps since -- 2 RB PDP + min(t, RB PDP)
-                constexpr int NPC = 2 * RB * PDP, NST = RB * PDP;
+                // in issue order): the 4 pieces of each of the RB * PDP items after it and the
+                // NJ stores of each loop step since -- 4 RB PDP + NJ min(t, RB PDP)
+                constexpr int NPC = 4 * RB * PDP, NST = NJ * RB * PDP;
                 static_assert(NPC + NST < 64, "vmcnt");
                 auto wait = [](auto Nc) {
                     constexpr int N = decltype(Nc)::value;
@@ -189,69 +240,53 @@ __global__ __launch_bounds__(HD_THREADS, 4) void k_hexresize_down(const Tin* __r
                     wait(std::integral_constant<int, NPC + NST>{});
                 } else {
                     fu_static_for<PDP>([&](auto Pc) {
-                        constexpr int P = decltype(Pc)::value;
-                        if (pi == P) wait(std::integral_constant<int, NPC + P * RB + k>{});
+                        constexpr int P_ = decltype(Pc)::value;
+                        if (pi == P_) wait(std::integral_constant<int, NPC + NJ * (P_ * RB + k)>{});
                     });
                 }
                 asm volatile("" ::: "memory");                    // LDS reads after the wait
-                const unsigned short* const s0 = base + 2 * k * WC;
-                const unsigned short* const s1 = s0 + WC;
+                const unsigned short* const s0 = base + 2 * k * RW;
+                const unsigned short* const s1 = s0 + RW;
                 float v[K];
 #pragma unroll
                 for (int kk = 0; kk < K; ++kk) {
                     const unsigned q = pk[k][kk];
-                    const unsigned short h1 = s0[q & 511];
-                    const unsigned short h2 = ((q >> 27) & 1) ? s1[(q >> 9) & 511] : s0[(q >> 9) & 511];
-                    const unsigned short h3 = s1[(q >> 18) & 511];
-                    const float v0 = ((q >> 28) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h1)) : 0.f;
-                    const float v1 = ((q >> 29) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h2)) : 0.f;
-                    const float v2 = ((q >> 30) & 1) ? to_acc<float>(__builtin_bit_cast(Tin, h3)) : 0.f;
+                    const float v0 = to_acc<float>(__builtin_bit_cast(Tin, s0[q & 1023]));
+                    const float v1 = to_acc<float>(__builtin_bit_cast(Tin, s0[(q >> 10) & 2047]));
+                    const float v2 = to_acc<float>(__builtin_bit_cast(Tin, s1[q >> 21]));
                     v[kk] = wt[k][kk][0] * v0 + wt[k][kk][1] * v1 + wt[k][kk][2] * v2;   // :354
                 }
-                if (full) {                                      // the lane's K columns at once
-                    if constexpr (sizeof(Tout) == 2) {
-                        unsigned pw[K / 2 > 0 ? K / 2 : 1];
 #pragma unroll
-                        for (int i = 0; i < K / 2; ++i) {
-                            typedef Tout t2v __attribute__((ext_vector_type(2)));
-                            pw[i] = __builtin_bit_cast(unsigned, t2v{from_acc<Tout>(v[2 * i]), from_acc<Tout>(v[2 * i + 1])});
-                        }
-                        if constexpr (K == 1)
-                            __builtin_amdgcn_raw_buffer_store_b16(
-                                __builtin_bit_cast(unsigned short, from_acc<Tout>(v[0])), yr, yo[k], yp, 0);
-                        else if constexpr (K == 2)
-                            __builtin_amdgcn_raw_buffer_store_b32(pw[0], yr, yo[k], yp, 0);
-                        else {
-                            typedef unsigned u2v __attribute__((ext_vector_type(2)));
-                            __builtin_amdgcn_raw_buffer_store_b64(u2v{pw[0], pw[1]}, yr, yo[k], yp, 0);
-                        }
-                    } else {
-                        if constexpr (K == 1) {
-                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[0]), yr, yo[k], yp, 0);
-                        } else if constexpr (K == 2) {
-                            typedef unsigned u2v __attribute__((ext_vector_type(2)));
-                            __builtin_amdgcn_raw_buffer_store_b64(
-                                u2v{__builtin_bit_cast(unsigned, v[0]), __builtin_bit_cast(unsigned, v[1])},
-                                yr, yo[k], yp, 0);
-                        } else {
-                            typedef unsigned u4v __attribute__((ext_vector_type(4)));
-                            __builtin_amdgcn_raw_buffer_store_b128(
-                                u4v{__builtin_bit_cast(unsigned, v[0]), __builtin_bit_cast(unsigned, v[1]),
-                                    __builtin_bit_cast(unsigned, v[2]), __builtin_bit_cast(unsigned, v[3])},
-                                yr, yo[k], yp, 0);
-                        }
-                    }
-                } else {   // the raster's last columns: one store per column (the extra stores
-                           // only over-count the waits above)
-#pragma unroll
-                    for (int kk = 0; kk < K; ++kk) {
-                        const unsigned o = (lane_live && bl + kk < D.w1) ? yo[k] + kk * (unsigned)sizeof(Tout)
-                                                                         : 0x80000000u;
+                for (int j = 0; j < NJ; ++j) {
+                    // lane 0 out of the window repeats store 0 (co[j] = b0): its values too
+                    const float v0 = rep[j] ? v[0] : v[P * j];
+                    const unsigned o = yo[k] + co[j];
+                    if constexpr (P == 1) {
                         if constexpr (sizeof(Tout) == 2)
                             __builtin_amdgcn_raw_buffer_store_b16(
-                                __builtin_bit_cast(unsigned short, from_acc<Tout>(v[kk])), yr, o, yp, 0);
+                                __builtin_bit_cast(unsigned short, from_acc<Tout>(v0)), yr, o, yp, 0);
                         else
-                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[kk]), yr, o, yp, 0);
+                            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v0), yr, o, yp, 0);
+                    } else {
+                        const float v1 = rep[j] ? v[1] : v[P * j + 1];
+                        if constexpr (sizeof(Tout) == 2) {
+                            typedef Tout t2v __attribute__((ext_vector_type(2)));
+                            __builtin_amdgcn_raw_buffer_store_b32(
+                                __builtin_bit_cast(unsigned, t2v{from_acc<Tout>(v0), from_acc<Tout>(v1)}), yr, o, yp, 0);
+                        } else {
+                            typedef unsigned u2v __attribute__((ext_vector_type(2)));
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                u2v{__builtin_bit_cast(unsigned, v0), __builtin_bit_cast(unsigned, v1)}, yr, o, yp, 0);
+                        }
+                        if (pc1[j]) {   // the raster's last column alone (extra stores only
+                                        // over-count the waits above)
+                            const unsigned o1 = yo[k] + (unsigned)(b0 + 2 * lane + 128 * j) * (unsigned)sizeof(Tout);
+                            if constexpr (sizeof(Tout) == 2)
+                                __builtin_amdgcn_raw_buffer_store_b16(
+                                    __builtin_bit_cast(unsigned short, from_acc<Tout>(v[P * j])), yr, o1, yp, 0);
+                            else
+                                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[P * j]), yr, o1, yp, 0);
+                        }
                     }
                 }
             });
@@ -285,27 +320,31 @@ static bool tsk_rows_ok(const Geom& g, double* qmin, double* qmax) {
     return true;
 }
 
-static bool tsk_lattice_ok(const Geom& g, int nout, int wc, double qmin, double qmax) {
+static bool tsk_lattice_ok(const Geom& g, int nout, int wc, int al, double qmin, double qmax) {
     const double cw = ((double)g.w - 0.5) * 0.5;
     const int64_t nwin = (g.w1 + nout - 1) / nout;
     for (int64_t wi = 0; wi < nwin; ++wi) {
         const int b0 = (int)(wi * nout);
         const int b1 = (int)std::min<int64_t>(b0 + nout, g.w1) - 1;
-        const int x0 = tsk_window_x0(g, qmin, b0, wc / 64);
+        const int x0 = tsk_window_x0(g, qmin, b0, al);
         const int hi = (int)floor(qmax + axis_at(g.ys, b1) + cw + 1e-6) + 2;
         if (hi - x0 > wc - 1) return false;
     }
     return true;
 }
 
-template <typename Tin, typename Tout, int K, int DB>
+template <typename Tin, typename Tout, int K, int DB, int P>
 static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st) {
     // resident waves: 256 CUs x 4 SIMDs x 4 waves; units split into plane chunks until
-    // there are >= 4 units per resident wave (the records are then recomputed per chunk)
+    // there are >= upw units per resident wave (the records are then recomputed per chunk:
+    // fewer, longer units amortise them, more units balance the waves; A/B switch
+    // HYGRID_TSK_UPW, default 1)
     constexpr int64_t RESIDENT = 256 * 4 * 4;
     constexpr int PDP = TsCfg<DB>::PDP;
+    const char* ue = getenv("HYGRID_TSK_UPW");
+    const int64_t upw = ue ? std::max(1, atoi(ue)) : 1;
     const int64_t tiles = (int64_t)D.nwin * D.nband;
-    int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, (4 * RESIDENT + tiles - 1) / tiles));
+    int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, (upw * RESIDENT + tiles - 1) / tiles));
     // a chunk's planes are one buffer each way: 32-bit offsets, including the planes past
     // the chunk the prefetch addresses (out of range: zeros)
     const int64_t plane_bytes = std::max<int64_t>((int64_t)D.h * D.w * 2, (int64_t)D.h1 * D.w1 * 4);
@@ -316,7 +355,7 @@ static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st)
     D.units = tiles * D.nchunk;
     const int64_t waves = std::min<int64_t>(D.units, RESIDENT);
     const unsigned blocks = (unsigned)((waves + 3) / 4);
-    hipLaunchKernelGGL((k_hexresize_down<Tin, Tout, K, DB>), dim3(blocks), dim3(HD_THREADS), 0, st,
+    hipLaunchKernelGGL((k_hexresize_down<Tin, Tout, K, DB, P>), dim3(blocks), dim3(HD_THREADS), 0, st,
                        (const Tin*)src, (Tout*)dst, D);
     return launch_status();
 }
@@ -340,20 +379,31 @@ int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t 
         return HG_EUNSUP;
     const Geom g = make_tri(h, w, h1, w1, op == HG_OP_HEXRESIZE ? 0.5 : 0.75);
     // input columns per output column: 512-column windows (16-B pieces) when downsampling,
-    // 128-column windows (4-B pieces) when upsampling or the rows are not 16-B aligned; lane
-    // l owns output columns K l .. K l + K - 1 of its window (K = 4, or 1 for narrow windows)
+    // 128-column windows (4-B pieces) when upsampling or the rows are not 16-B aligned; a
+    // lane owns K output columns of its window in groups of P adjacent ones (K = 4, or
+    // fewer for narrow windows)
     const double ratio = w1 > 1 ? (double)(w - 1) / (double)(w1 - 1) : 1.0;
-    const int DB = (ratio >= 0.75 && a16) ? 16 : 4, wc = 32 * DB;
+    const int DB = (ratio >= 0.75 && a16) ? 16 : 4, wc = 32 * DB + 16, al = DB / 2;
+    const int P = DB == 16 ? HD_P16 : HD_P4;
+    if (P == 2 && w1 < 2) return HG_EUNSUP;
     HexDownGeom D = {};
     double qmax;
     if (!tsk_rows_ok(g, &D.qmin, &qmax)) return HG_EUNSUP;
+    // output windows of whole 128-B lines when the lattice allows (64 16-bit or 32 fp32
+    // columns: partial lines shared by two waves cost ~10-20 %, measured), else the widest
     int nout = std::min(256, (int)std::floor((wc - 6) / std::max(ratio, 1e-3)));
-    for (; nout >= 32; --nout) {
-        if (nout > 64 && (nout & 3)) continue;       // whole lanes of K = 4
-        if (tsk_lattice_ok(g, nout, wc, D.qmin, qmax)) break;
+    if (const char* ne = getenv("HYGRID_TSK_NOUT")) nout = std::min(nout, atoi(ne));   // A/B switch
+    const int L = ddt == HG_F32 ? 32 : 64;
+    int best = 0;
+    for (int n = nout / L * L; n >= L && !best; n -= L)
+        if (tsk_lattice_ok(g, n, wc, al, D.qmin, qmax) && !(P == 2 && w1 % n == 1)) best = n;
+    for (int n = nout; n >= 32 && !best; --n) {
+        if (P == 2 && ((n & 1) || w1 % n == 1)) continue;   // >= 2 columns per window
+        if (tsk_lattice_ok(g, n, wc, al, D.qmin, qmax)) best = n;
     }
-    if (nout < 32) return HG_EUNSUP;                  // > ~15x downsampling: the general kernel
-    const int K = nout > 64 ? 4 : 1;
+    if (!best) return HG_EUNSUP;                       // > ~15x downsampling: the general kernel
+    nout = best;
+    const int K = nout > 64 * P ? 4 : P;
     D.g = g;
     D.planes = planes;
     D.h = (int)h; D.w = (int)w; D.h1 = (int)h1; D.w1 = (int)w1;
@@ -363,8 +413,10 @@ int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t 
                     (DB == 16 ? TsCfg<16>::RB : TsCfg<4>::RB));
     if (dry) return HG_OK;
 #define HG_TSK(TI, TO)                                                                         \
-    if (DB == 4) return K == 4 ? hd_launch<TI, TO, 4, 4>(src, dst, D, st) : hd_launch<TI, TO, 1, 4>(src, dst, D, st); \
-    return K == 4 ? hd_launch<TI, TO, 4, 16>(src, dst, D, st) : hd_launch<TI, TO, 1, 16>(src, dst, D, st);
+    if (DB == 4) return K == 4 ? hd_launch<TI, TO, 4, 4, HD_P4>(src, dst, D, st)               \
+                               : hd_launch<TI, TO, HD_P4, 4, HD_P4>(src, dst, D, st);          \
+    return K == 4 ? hd_launch<TI, TO, 4, 16, HD_P16>(src, dst, D, st)                           \
+                  : hd_launch<TI, TO, HD_P16, 16, HD_P16>(src, dst, D, st);
     if (sdt == HG_BF16) {
         if (ddt == HG_BF16) { HG_TSK(__bf16, __bf16) }
         if (ddt == HG_F16) { HG_TSK(__bf16, _Float16) }

@@ -55,11 +55,12 @@ def test_same_size_keeps_its_kernels():
     # odd input widths (rows not dword-aligned for LDS-DMA) keep the general kernel
     assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 33, 125, 16, 62,
                    _abi.HG_LINEAR) == _abi.HG_KERNEL_GENERAL
-    # any ratio whose window of >= 16 output columns keeps its vertices in 128 input columns
-    # (4x: 30 columns per wave); 16x does not fit
-    assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 2160, 3840, 540, 960,
-                   _abi.HG_LINEAR) == _abi.HG_KERNEL_DOWN
-    assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 2160, 3840, 135, 240,
+    # any ratio whose window of >= 32 output columns keeps its vertices in the wave's 528
+    # input columns (4x: 128 columns per wave, 16x: 32); 32x does not fit
+    for h1, w1 in ((540, 960), (135, 240)):
+        assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 2160, 3840, h1, w1,
+                       _abi.HG_LINEAR) == _abi.HG_KERNEL_DOWN
+    assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 2160, 3840, 68, 120,
                    _abi.HG_LINEAR) == _abi.HG_KERNEL_GENERAL
     # hex (h/2, w/2) -> rect (h, w), the inverse of ConvertToHexagon's lattice: the same
     # streaming triangle kernel (two output columns per lane); fp64 out keeps the general one

@@ -110,6 +110,34 @@ def test_hexresize_pyramid_levels_full_size(B, C, h, w):
             assert np.abs(got - ref).max() <= 2.0 ** -11 * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("h,w,h1,w1", [(256, 1024, 64, 256), (256, 1024, 32, 128),
+                                       (512, 2048, 32, 128), (130, 520, 26, 104)])
+def test_hexresize_strong_downsampling(h, w, h1, w1):
+    """4x / 8x / 16x / 5x: narrower windows (K = 4 down to 1 column per lane) on the same
+    kernel, bit-identical to the general kernel and within one rounding of the oracle."""
+    g = torch.Generator(device=DEV).manual_seed(h1 * 7 + w1)
+    x = torch.rand((2, 3, h, w), generator=g, device=DEV).to(torch.float16)
+    assert _kernel(x, (h1, w1), torch.float16) == _abi.HG_KERNEL_DOWN
+    y = ops.hexresize(x, (h1, w1), out_dtype=torch.float16)
+    torch.cuda.synchronize()
+    _same_bits(y, _general(ops.hexresize, x, (h1, w1), out_dtype=torch.float16))
+    ref = O.hexresize(x[1].double().cpu().numpy(), (h1, w1), 1)
+    assert np.abs(y[1].double().cpu().numpy() - ref).max() <= 2.0 ** -11 * np.abs(ref).max()
+
+
+def test_hexresize_base_not_16b_aligned():
+    """A source 4-B but not 16-B aligned takes the 4-B-piece configuration (128 + 16 input
+    columns per wave); results bit-identical to the general kernel."""
+    h, w = 96, 512
+    flat = torch.rand(2 * 3 * h * w + 2, device=DEV).to(torch.bfloat16)
+    x = flat[2:].view(2, 3, h, w)
+    assert x.data_ptr() % 16 == 4
+    for od in (torch.bfloat16, torch.float32):
+        y = ops.hexresize(x, (h // 2, w // 2), out_dtype=od)
+        torch.cuda.synchronize()
+        _same_bits(y, _general(ops.hexresize, x, (h // 2, w // 2), out_dtype=od))
+
+
 def test_hexresize_nonfinite_bit_identical():
     """NaN / Inf inputs (raster corners and edges, window and unit boundaries) reach exactly
     the outputs the general kernel's taps reach."""
@@ -127,13 +155,13 @@ def test_hexresize_nonfinite_bit_identical():
 
 def test_hexresize_outside_domain_keeps_general_kernel():
     """fp32 inputs, fp64 outputs (the NumPy API's bit-exact path), odd input widths and ratios
-    whose window of 16 output columns no longer fits 128 input columns stay on the general
-    kernel."""
+    whose window of 32 output columns no longer fits the wave's input columns stay on the
+    general kernel."""
     x = torch.rand((1, 1, 64, 66), device=DEV)
     assert _kernel(x, (32, 33), torch.float32) == _abi.HG_KERNEL_GENERAL
     xh = x.half()
     assert _kernel(xh, (32, 33), torch.float64) == _abi.HG_KERNEL_GENERAL
-    assert _kernel(xh, (4, 4), torch.float16) == _abi.HG_KERNEL_GENERAL     # 16x
+    assert _kernel(xh, (4, 4), torch.float16) == _abi.HG_KERNEL_GENERAL     # 16x, 4-B pieces
     # odd input widths: rows not dword-aligned for LDS-DMA
     xo = torch.rand((1, 1, 33, 125), device=DEV).half()
     assert _kernel(xo, (16, 62), torch.float16) == _abi.HG_KERNEL_GENERAL

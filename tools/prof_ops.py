@@ -5,7 +5,8 @@ usage: python tools/prof_ops.py OP [iters]
   rt   config 2: fused rect -> hex -> rect round trip, 1080p fp32 b32 (k_fused MD 2)
   pyr0 config 5 level 0 from the rect image, 8K fp16 b8 (k_fused MD 3)
   pyr1 config 5 level 1 (4K -> 2K from a hex image)
-  hr0  hexresize 8K -> 4K fp16 b8 (the pyramid chain's level-0 hexresize)
+  hr0  hexresize 8K -> 4K fp16 b8 (the pyramid chain's level-0 hexresize); hr1 4K -> 2K,
+       hr2 2K -> 1K (levels 1, 2)
   up   hex (1080, 1920) -> rect (2160, 3840) bf16 b32
 """
 import os
@@ -34,9 +35,10 @@ def main():
         H, W = shape[-2:]
         fn = lambda: ops.hex_pyramid_level(x, taps, None, (H // 2, W // 2), 0,  # noqa: E731
                                            from_rect=(op == "pyr0"), out_dtype=torch.float16)
-    elif op == "hr0":
-        x = torch.rand((8, 3, 4320, 7680), device=dev, dtype=torch.float16)
-        fn = lambda: ops.hexresize(x, (2160, 3840), out_dtype=torch.float16)  # noqa: E731
+    elif op in ("hr0", "hr1", "hr2"):
+        H, W = {"hr0": (4320, 7680), "hr1": (2160, 3840), "hr2": (1080, 1920)}[op]
+        x = torch.rand((8, 3, H, W), device=dev, dtype=torch.float16)
+        fn = lambda: ops.hexresize(x, (H // 2, W // 2), out_dtype=torch.float16)  # noqa: E731
     elif op == "up":
         x = torch.rand((32, 3, 1080, 1920), device=dev, dtype=torch.bfloat16)
         fn = lambda: ops.hex_to_rect(x, (2160, 3840))  # noqa: E731

@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 tail -15 $OUT/pytest.log
 [ $rc -eq 0 ] || exit $rc
 for op in hr0 hr1 hr2 up; do
-  timeout -k 10 200 python tools/ab_ops.py $op 8 base base%HYGRID_DOWN=0 >> $OUT/ab_ops.txt 2>&1 || exit 1
+  timeout -k 10 200 python tools/ab_ops.py $op 8 base base%HYGRID_TSK_UPW=4 base%HYGRID_DOWN=0 >> $OUT/ab_ops.txt 2>&1 || exit 1
 done
 cat $OUT/ab_ops.txt
 for op in pyrfr pyr1 pyr2; do
