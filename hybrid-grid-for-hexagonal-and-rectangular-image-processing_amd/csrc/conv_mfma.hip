@@ -330,6 +330,256 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16(const __bf16* 
         }
 }
 
+// ---- bf16 inputs, staging by LDS-DMA (round 4) -------------------------------------------
+// The same GEMM and fragment maps as k_hexconv_mfma_bf16, with the staging taken off the
+// critical path: (1) the three bf16 weight parts are split once per call by k_wsplit_bf16
+// into a stream-ordered scratch buffer already in the LDS fragment layout, so a workgroup's
+// weight chunk is a plain 1-KiB-piece LDS-DMA copy (double-buffered: chunk i + 1 lands while
+// chunk i's MFMAs run); (2) P's rows arrive by LDS-DMA in their natural [channel][row][col]
+// order (one dword per lane, 40 lanes = 80 columns per piece), also one chunk ahead, and a
+// short LDS -> LDS pass packs them channel-innermost for the ds_read_b128 B fragments.  No
+// staging value passes through VGPRs, so the prefetch costs no occupancy (the register
+// prefetch of round 3 did: 2 waves per SIMD, 27 % slower).  Workgroups whose P tile needs
+// padding or the type1 structural zero column keep the register staging for P.
+constexpr int CD_PRW = 40;                    // raw P row: 40 dwords = 80 columns (>= 72 + 1)
+constexpr int CD_PRAW = CM_CC * CM_PR * CD_PRW;   // dwords of one raw P chunk
+
+// one block per (chunk of 8 input channels, 16 output channels); thread (o, t) splits the
+// 8 channels' weights of tap t (t = 7: zeros) into h + m + l and stores the three fragments;
+// flag[chunk][o / 16] = some m / l part is nonzero (else the MFMA kernel skips parts 2, 3)
+__global__ __launch_bounds__(128) void k_wsplit_bf16(const float* __restrict__ kern, cm_u4* __restrict__ wf,
+                                                     int* __restrict__ flag, int C, int O, int Opad) {
+    const int ci = blockIdx.x, ob = blockIdx.y;
+    const int o = ob * 16 + (threadIdx.x >> 3), t = threadIdx.x & 7;
+    unsigned short h[8], m[8], l[8];
+    int ml = 0;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) {
+        const int c = ci * 8 + cc;
+        const float wv = (t < 7 && o < O && c < C) ? kern[((int64_t)o * C + c) * 7 + t] : 0.f;
+        const __bf16 bh = (__bf16)wv;
+        const float r1 = wv - (float)bh;
+        const __bf16 bm = (__bf16)r1;
+        const __bf16 bl = (__bf16)(r1 - (float)bm);
+        h[cc] = __builtin_bit_cast(unsigned short, bh);
+        m[cc] = __builtin_bit_cast(unsigned short, bm);
+        l[cc] = __builtin_bit_cast(unsigned short, bl);
+        ml |= (m[cc] | l[cc]) & 0x7fff;
+    }
+    auto pk = [](const unsigned short* u) {
+        return cm_u4{u[0] | ((unsigned)u[1] << 16), u[2] | ((unsigned)u[3] << 16),
+                     u[4] | ((unsigned)u[5] << 16), u[6] | ((unsigned)u[7] << 16)};
+    };
+    const int kb = t >> 2, g = t & 3;
+    auto at = [&](int pt) { return ((((int64_t)ci * 3 + pt) * 2 + kb) * Opad + o) * 4 + g; };
+    wf[at(0)] = pk(h);
+    wf[at(1)] = pk(m);
+    wf[at(2)] = pk(l);
+    const int any = __syncthreads_or(ml != 0);
+    if (threadIdx.x == 0) flag[ci * (Opad / 16) + ob] = any;
+}
+
+template <int N>
+__device__ __forceinline__ void cd_wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf) | ((N >> 4) << 14));
+}
+
+template <typename Tout, int NOT>
+__global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
+                                                                   const cm_u4* __restrict__ wf,
+                                                                   const int* __restrict__ flag,
+                                                                   const float* __restrict__ bias,
+                                                                   Tout* __restrict__ y, MfmaGeom G,
+                                                                   int Opad) {
+    constexpr int CM_O = 16 * NOT;
+    constexpr int WSZ = 3 * 2 * CM_O * 4;                // weight fragments of one chunk
+    constexpr int WPC = WSZ / 64;                         // their 1-KiB pieces
+    constexpr int WPW = WPC / 4;                          // ... per wave
+    constexpr int PPW = CM_CC * CM_PR / 4;                // raw P row pieces per wave (12)
+    static_assert(WPC % 4 == 0, "pieces");
+    // one LDS array (so the DMA's M0 bases come from it): [psb | wsb x 2 | praw x 2]
+    constexpr int LPSB = CB_PSZ * 16, LWSB = WSZ * 16, LPRAW = CD_PRAW * 4;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LPSB + 2 * LWSB + 2 * LPRAW];
+    cm_u4* const psb = reinterpret_cast<cm_u4*>(lds);
+    const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    unsigned bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int tq = (int)(bid % G.ntq); bid /= G.ntq;
+    const int tr = (int)(bid % G.ntr); bid /= G.ntr;
+    const int to = (int)(bid % G.nto);
+    const int64_t b = bid / G.nto;
+    const int q0 = tq * CM_Q, r0 = tr * CM_ROWS, o0 = to * CM_O;
+    const int r = r0 + wv;
+    const int par = r & 1;
+    const int Wp = G.w + 2 * G.p, Hp = G.h + 2 * G.p;
+    const int li = lane & 15, lg = lane >> 4;
+    const unsigned short padv = __builtin_bit_cast(unsigned short, (__bf16)G.pad_value);
+    const int nch = (G.C + CM_CC - 1) / CM_CC;
+    // this tile's P is all inside the image (no padding, no structural zero): DMA staging
+    const int px0 = q0 + G.mink - G.p;                    // first staged source column
+    const bool interior = r0 - G.p >= 0 && r0 + CM_PR - 1 - G.p < G.h && px0 >= 0 &&
+                          px0 + CB_PP - 1 < G.w && q0 + G.mink + CB_PP - 1 < Wp;
+    const int xs = px0 & ~1, sh = px0 - xs;               // dword-aligned raw start, shift
+
+    cm_f4 acc[NOT][4];
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int o = o0 + ot * 16 + lg * 4 + v;
+            const float bv = (bias && o < G.O) ? bias[o] : 0.f;
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt) acc[ot][qt][v] = bv;
+        }
+    }
+    if (tid == 0) psb[CB_PSZ - 1] = cm_u4{0u, 0u, 0u, 0u};
+    int pidx[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        const int t = 4 * kb + lg;
+        pidx[kb] = t < 7 ? (wv + G.dy[t]) * CB_PP + li + (par ? G.dk[1][t] : G.dk[0][t]) : -1;
+    }
+    const unsigned short* xb = reinterpret_cast<const unsigned short*>(x) + b * (int64_t)G.C * G.h * G.w;
+    // buffer views: the image's planes (rows of channels >= C read past the range: zeros),
+    // the weight fragments
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)xb, (short)0, (int)((int64_t)G.C * G.h * G.w * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)wf, (short)0, 0x7fffffff, 0x00020000);
+
+    auto dma = [&](int ci) {                              // chunk ci -> buffers (ci & 1)
+        const int buf = ci & 1;
+        // weights: pieces j = wv * WPW + i of the chunk's (pt, kb) blocks of CM_O * 4 fragments
+#pragma unroll
+        for (int i = 0; i < WPW; ++i) {
+            const int j = wv * WPW + i;
+            const int blk = j / (CM_O / 16), part = j % (CM_O / 16);   // (pt * 2 + kb), 1-KiB part
+            const unsigned so = (unsigned)((((int64_t)ci * 6 + blk) * Opad + o0) * 64 + part * 1024);
+            const unsigned lda = lds0 + LPSB + buf * LWSB + (blk * CM_O * 4) * 16 + part * 1024;
+            const unsigned vo = lane * 16u;
+            unsigned keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                         "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(vo), "s"(wr), "s"(lda), "s"(so) : "memory");
+        }
+        if (interior) {
+            // P rows: pieces j = wv * PPW + i = (cc, pr); lanes 0-39 one dword each
+#pragma unroll
+            for (int i = 0; i < PPW; ++i) {
+                const int j = wv * PPW + i;
+                const int cc = j / CM_PR, pr = j % CM_PR;
+                const int c = ci * CM_CC + cc;
+                const unsigned so = c < G.C ? (unsigned)((((int64_t)c * G.h + (r0 + pr - G.p)) * G.w + xs) * 2)
+                                            : 0x80000000u;
+                const unsigned lda = lds0 + LPSB + 2 * LWSB + buf * LPRAW + j * CD_PRW * 4;
+                const unsigned vo = lane * 4u;
+                unsigned keep;
+                if (lane < CD_PRW)
+                    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                                 "buffer_load_dword %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+                                 : "=&s"(keep) : "v"(vo), "s"(xr), "s"(lda), "s"(so) : "memory");
+                else
+                    asm volatile("" ::: "memory");
+            }
+        }
+    };
+    // every wave issues the same number of DMA instructions per chunk (counted waits)
+    constexpr int NW = WPW, NP_ = PPW;
+
+    dma(0);
+    for (int ci = 0; ci < nch; ++ci) {
+        const int buf = ci & 1;
+        const int c0 = ci * CM_CC;
+        if (ci + 1 < nch) {
+            dma(ci + 1);
+            if (interior) cd_wait_vm<NW + NP_>(); else cd_wait_vm<NW>();
+        } else {
+            cd_wait_vm<0>();
+        }
+        // ---- P chunk -> psb (channel-innermost fragments) -------------------------------
+        if (interior) {
+            __builtin_amdgcn_s_barrier();                 // every wave's raw rows have landed
+            const unsigned short* raw = reinterpret_cast<const unsigned short*>(lds + LPSB + 2 * LWSB + buf * LPRAW);
+            for (int f = tid; f < CM_PR * CB_PP; f += CM_THREADS) {
+                const int pr = f / CB_PP, pc = f - pr * CB_PP;
+                unsigned short v[8];
+#pragma unroll
+                for (int cc = 0; cc < 8; ++cc) v[cc] = raw[(cc * CM_PR + pr) * (2 * CD_PRW) + pc + sh];
+                psb[f] = cm_u4{v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
+                               v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16)};
+            }
+        } else if (tid < 3 * CB_PP) {                     // the register staging (padding rules)
+            const int pc = tid % CB_PP, ph = tid / CB_PP;
+            const int px = q0 + G.mink + pc;
+            const bool zc = px >= Wp;
+            const int64_t xi = zc ? -1 : pad_map(px - G.p, G.w, G.pad_mode);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int pr = ph + 3 * k, py = r0 + pr;
+                const int64_t yi = (!zc && py < Hp) ? pad_map(py - G.p, G.h, G.pad_mode) : -1;
+                unsigned short v[8];
+#pragma unroll
+                for (int cc = 0; cc < 8; ++cc) {
+                    const int c = c0 + cc;
+                    unsigned short e = 0;
+                    if (!zc && c < G.C && py < Hp)
+                        e = (yi < 0 || xi < 0) ? padv : xb[((int64_t)c * G.h + yi) * G.w + xi];
+                    v[cc] = e;
+                }
+                psb[pr * CB_PP + pc] = cm_u4{v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
+                                             v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16)};
+            }
+        }
+        int nparts = 1;
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) nparts |= flag[ci * (Opad / 16) + o0 / 16 + ot] ? 3 : 1;
+        __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): this wave's LDS writes
+        __builtin_amdgcn_s_barrier();                     // psb and the weights complete
+        // ---- 2 k blocks x 4 column tiles x 3 weight parts x NOT channel tiles -------------
+        const cm_u4* const wsb = reinterpret_cast<const cm_u4*>(lds + LPSB + buf * LWSB);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            cm_b8 bf[4];
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt)
+                bf[qt] = __builtin_bit_cast(cm_b8, psb[pidx[kb] < 0 ? CB_PSZ - 1 : pidx[kb] + qt * 16]);
+#pragma unroll
+            for (int pt = 0; pt < 3; ++pt) {
+                if (pt >= nparts) break;
+#pragma unroll
+                for (int ot = 0; ot < NOT; ++ot) {
+                    const cm_b8 af = __builtin_bit_cast(cm_b8, wsb[((pt * 2 + kb) * CM_O + ot * 16 + li) * 4 + lg]);
+#pragma unroll
+                    for (int qt = 0; qt < 4; ++qt)
+                        acc[ot][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[qt], acc[ot][qt], 0, 0, 0);
+                }
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_s_barrier();                     // psb / this buffer free again
+    }
+
+    if (r >= G.ho) return;
+    Tout* yb = y + b * (int64_t)G.O * G.ho * G.wo;
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int o = o0 + ot * 16 + lg * 4 + v;
+            if (o >= G.O) continue;
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt) {
+                const int q = q0 + qt * 16 + li;
+                if (q >= G.wo) continue;
+                float val = acc[ot][qt][v];
+                if (G.epi.on) val = epi_apply(val, o, G.epi);
+                yb[((int64_t)o * G.ho + r) * G.wo + q] = (Tout)val;
+            }
+        }
+}
+
 // Runs the MFMA kernel when it covers the call and pays (dense radius-2, stride-1,
 // dilation-1 conv with C >= 8 and O >= 16, f32 weights); HG_EUNSUP otherwise.
 int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_dtype,
@@ -375,6 +625,28 @@ int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_
     // A/B switch HYGRID_CONV_MFMA_BF16=0: the f32 kernel
     if (x_dtype == HG_BF16 && bf_pad && !env_is("HYGRID_CONV_MFMA_BF16", "0") &&
         (y_dtype == HG_BF16 || y_dtype == HG_F32)) {
+        // LDS-DMA staging (A/B switch HYGRID_CONV_DMA=0: the register-staged kernel below):
+        // rows must be dword-aligned (even width, 4-B aligned base)
+        if (!env_is("HYGRID_CONV_DMA", "0") && (G.w % 2) == 0 && (reinterpret_cast<uintptr_t>(x) & 3) == 0) {
+            const int nch = (G.C + CM_CC - 1) / CM_CC, Opad = G.nto * 16 * nt;
+            const size_t wbytes = (size_t)nch * 6 * Opad * 64, fbytes = (size_t)nch * (Opad / 16) * 4;
+            void* ws = nullptr;
+            hipError_t e = hipMallocAsync(&ws, wbytes + fbytes, st);
+            if (e != hipSuccess) return (int)e;
+            cm_u4* wfr = static_cast<cm_u4*>(ws);
+            int* flg = reinterpret_cast<int*>(static_cast<char*>(ws) + wbytes);
+            hipLaunchKernelGGL(k_wsplit_bf16, dim3(nch, Opad / 16), dim3(128), 0, st, k, wfr, flg, G.C, G.O, Opad);
+#define HG_CD_LAUNCH(TO)                                                                      \
+            if (nt == 2)                                                                      \
+                hipLaunchKernelGGL((k_hexconv_mfma_bf16d<TO, 2>), grid, blk, 0, st, (const __bf16*)x, wfr, flg, b, (TO*)y, G, Opad); \
+            else                                                                              \
+                hipLaunchKernelGGL((k_hexconv_mfma_bf16d<TO, 4>), grid, blk, 0, st, (const __bf16*)x, wfr, flg, b, (TO*)y, G, Opad);
+            if (y_dtype == HG_BF16) { HG_CD_LAUNCH(__bf16) } else { HG_CD_LAUNCH(float) }
+#undef HG_CD_LAUNCH
+            const int ls = launch_status();
+            const hipError_t fe = hipFreeAsync(ws, st);
+            return ls != HG_OK ? ls : (int)fe;
+        }
 #define HG_CB_LAUNCH(TO)                                                                      \
         if (nt == 2)                                                                          \
             hipLaunchKernelGGL((k_hexconv_mfma_bf16<TO, 2>), grid, blk, 0, st, (const __bf16*)x, k, b, (TO*)y, G); \

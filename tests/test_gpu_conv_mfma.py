@@ -225,3 +225,61 @@ def test_mfma_bf16_exact_weights_keep_inf():
     assert torch.equal(y[torch.isinf(ref)], ref[torch.isinf(ref)])
     fin = torch.isfinite(ref)
     torch.testing.assert_close(y[fin], ref[fin], rtol=1e-5, atol=1e-5 * float(ref[fin].abs().max()))
+
+
+# ---- bf16 inputs staged by LDS-DMA (k_hexconv_mfma_bf16d, round 4) ------------------------
+
+def _with_env(name, value, fn, *args, **kw):
+    old = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        out = fn(*args, **kw)
+        torch.cuda.synchronize()
+        return out
+    finally:
+        if old is None:
+            del os.environ[name]
+        else:
+            os.environ[name] = old
+
+
+DMA_CASES = [  # (B, C, O, h, w): interior tiles (DMA-staged P) and border tiles in each
+    (1, 64, 64, 40, 300), (2, 13, 20, 30, 260), (1, 70, 33, 17, 202), (1, 24, 100, 21, 196),
+    (1, 8, 16, 12, 140)]
+
+
+@pytest.mark.parametrize("case", DMA_CASES)
+@pytest.mark.parametrize("pad", [0, 1, 2])
+@pytest.mark.parametrize("off", [0, 1])
+def test_mfma_bf16_dma_bit_identical_to_register_staging(case, pad, off):
+    """The LDS-DMA-staged kernel issues the register-staged kernel's MFMAs on the same
+    fragments in the same order: outputs bit-identical (HYGRID_CONV_DMA=0 selects the latter),
+    bf16 and fp32 outputs, partial channel chunks and output-channel tiles included."""
+    B, C, O_, h, w = case
+    k, b = _weights(O_, C, h * 7 + w + pad)
+    x = _bf16_input((B, C, h, w), h + w + off)
+    for od in (torch.float32, torch.bfloat16):
+        y = ops.hexconv2d(x, k, b, off, 2, padding=pad, out_dtype=od)
+        torch.cuda.synchronize()
+        ref = _with_env("HYGRID_CONV_DMA", "0", ops.hexconv2d, x, k, b, off, 2, padding=pad, out_dtype=od)
+        assert torch.equal(y.view(torch.int16 if od == torch.bfloat16 else torch.int32),
+                           ref.view(torch.int16 if od == torch.bfloat16 else torch.int32))
+
+
+def test_mfma_bf16_dma_vs_oracle_and_unaligned():
+    """1e-5 against the fp64 oracle on a shape with many interior tiles; a source that is
+    2-B aligned only (odd element offset) keeps the register staging, same results."""
+    B, C, O_, h, w = 1, 32, 48, 36, 330
+    k, b = _weights(O_, C, 77)
+    x = _bf16_input((B, C, h, w), 31)
+    y = ops.hexconv2d(x, k, b, 0, 2, padding=1, out_dtype=torch.float32)
+    ref = O.hexconv2d(x.double().cpu().numpy(), k.cpu().double().numpy(),
+                      b.cpu().double().numpy(), 0, 2, padding=1)
+    scale = max(np.abs(ref).max(), 1e-30)
+    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=1e-5, atol=1e-5 * scale)
+    flat = torch.empty(B * C * h * w + 1, device=DEV, dtype=torch.bfloat16)
+    xu = flat[1:].view(B, C, h, w)
+    xu.copy_(x)
+    yu = ops.hexconv2d(xu, k, b, 0, 2, padding=1, out_dtype=torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(yu, y)
