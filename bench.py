@@ -209,6 +209,9 @@ def bench_lattices(ops, measure, gen, dev, world, Bl, C, H, W):
               "Image.py:111-116: rect->hex (h//2, w//2) nearest, u8"),
              ("r2h_bilinear_2x", "rect_to_hex", xbf, 1, 2, (hs, ws),
               "geometry_np.py:772-776 ratio: rect->hex (h//2, w//2) bilinear, bf16"),
+             ("hexresize_2x", "hexresize", xbf, 1, 2, (hs, ws),
+              "geometry_np.py:520-681: hexresize hex (h, w) -> hex (h//2, w//2) linear, bf16 "
+              "(one pyramid level's resample alone)"),
              ("h2r_linear_2x_up", "hex_to_rect", hbf, 1, 2, (H, W),
               "geometry_np.py:191-356: hex (h//2, w//2) -> rect (h, w) linear, bf16 (inverse of "
               "ConvertToHexagon's lattice)"),

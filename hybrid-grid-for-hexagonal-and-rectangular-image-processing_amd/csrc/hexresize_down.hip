@@ -53,7 +53,13 @@ __device__ __forceinline__ void fu_static_for(F&& f) {
 #define HD_PDP16 1          // 16-B pieces: planes in flight ahead of the one blended
 #endif
 #ifndef HD_RB4
-#define HD_RB4 2
+#define HD_RB4 4
+#endif
+#ifndef HD_NR16
+#define HD_NR16 4           // 16-B pieces: input rows loaded per (unit, plane) (host-checked)
+#endif
+#ifndef HD_NR4
+#define HD_NR4 4
 #endif
 #ifndef HD_PDP4
 #define HD_PDP4 2
@@ -76,8 +82,8 @@ constexpr int HD_THREADS = 256;
 // 32-B piece of 8 lanes), rows per unit, planes ahead; a ring row holds the window's WC
 // samples and a 16-B zero slot (the vertices outside the raster read it)
 template <int DB> struct TsCfg;
-template <> struct TsCfg<4> { static constexpr int WC = 144, RB = HD_RB4, PDP = HD_PDP4; };
-template <> struct TsCfg<16> { static constexpr int WC = 528, RB = HD_RB16, PDP = HD_PDP16; };
+template <> struct TsCfg<4> { static constexpr int WC = 144, RB = HD_RB4, NR = HD_NR4, PDP = HD_PDP4; };
+template <> struct TsCfg<16> { static constexpr int WC = 528, RB = HD_RB16, NR = HD_NR16, PDP = HD_PDP16; };
 
 struct HexDownGeom {
     Geom g;                       // make_tri(h, w, h1, w1, margin)
@@ -108,20 +114,24 @@ __host__ __device__ inline int tsk_window_x0(const Geom& g, double qmin, int b0,
     return lo >= 0 ? lo - lo % al : -(((-lo) + al - 1) / al * al);
 }
 
-template <typename Tin, typename Tout, int K, int DB, int P>
+template <typename Tin, typename Tout, int K, int DB, int P, bool SEP>
 __global__ __launch_bounds__(HD_THREADS, HD_WPE) void k_hexresize_down(const Tin* __restrict__ x,
                                                                Tout* __restrict__ y,
                                                                HexDownGeom D) {
     static_assert(sizeof(Tin) == 2, "16-bit inputs");
-    constexpr int WC = TsCfg<DB>::WC, RB = TsCfg<DB>::RB, PDP = TsCfg<DB>::PDP, NP = PDP + 1;
+    // SEP: every output row loads its own two input rows (strong downsampling: the band's
+    // rows share none), else the band's NR consecutive rows are loaded once per plane
+    constexpr int WC = TsCfg<DB>::WC, RB = TsCfg<DB>::RB, PDP = TsCfg<DB>::PDP;
+    constexpr int NR = SEP ? 2 * RB : TsCfg<DB>::NR;
+    constexpr int NP = PDP + 1;
     constexpr int ROWB = WC * 2 + 16;                         // ring bytes of one input row
     constexpr int RW = ROWB / 2;                              // the same in samples
-    static_assert(NP * RB * 2 * ROWB <= HD_RING && WC < 1024 && 2 * RW < 2048, "ring");
+    static_assert(NP * NR * ROWB <= HD_RING && WC < 1024 && 2 * RW < 2048, "ring");
     __shared__ __attribute__((aligned(16))) unsigned char ring_all[HD_THREADS / 64][HD_RING];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     unsigned char* const ring = ring_all[wslot];
-    if (lane < NP * RB * 2) {                                 // the zero slots (never DMA'd)
+    if (lane < NP * NR) {                                     // the zero slots (never DMA'd)
         typedef unsigned u4v __attribute__((ext_vector_type(4)));
         *reinterpret_cast<u4v*>(ring + lane * ROWB + 2 * WC) = u4v{0u, 0u, 0u, 0u};
     }
@@ -195,19 +205,20 @@ __global__ __launch_bounds__(HD_THREADS, HD_WPE) void k_hexresize_down(const Tin
             pc1[j] = P == 2 && !all && c < bend;
         }
 
-        // ---- (plane, row) items: LDS-DMA of rows i_n, i_n + 1 of plane pi + PDP ----------
+        // ---- per plane: LDS-DMA of the NR input rows rlo .. rlo + NR - 1 the band's output
+        // rows read (rows i_n, i_n + 1 of each; host-checked to fit), PDP planes ahead ------
         // (columns left of the raster: the lane's piece is clamped to column 0 and every
-        // vertex there is outside the raster, masked by vk)
+        // vertex there is outside the raster, read from the zero slot)
+        const int rlo = r0[0];
         const unsigned voff = (unsigned)max(xb + (DB / 2) * lane, 0) * 2u;
         const unsigned voff2 = (unsigned)max(xb + 32 * DB + 2 * lane, 0) * 2u;
-        auto slots = [&](int pi) { return ring + (pi % NP) * (2 * RB * ROWB); };
-        auto dma = [&](int pi, auto Kc) {
-            constexpr int k = decltype(Kc)::value;
-            unsigned char* const sl = slots(pi) + 2 * k * ROWB;
+        auto slots = [&](int pi) { return ring + (pi % NP) * (NR * ROWB); };
+        auto dma = [&](int pi) {
+            unsigned char* const sl = slots(pi);
             const unsigned po = pi < np ? (unsigned)pi * planeb : (unsigned)np * planeb;
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const unsigned so = po + (unsigned)(r0[k] + q) * rowb;
+            for (int q = 0; q < NR; ++q) {
+                const unsigned so = po + (unsigned)(SEP ? r0[q / 2] + q % 2 : rlo + q) * rowb;
                 auto* const ld = (__attribute__((address_space(3))) void*)(sl + q * ROWB);
                 if constexpr (DB == 16)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, ld, 16, voff, so, 0, 0);
@@ -218,34 +229,35 @@ __global__ __launch_bounds__(HD_THREADS, HD_WPE) void k_hexresize_down(const Tin
                 if (lane < 8) __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, le, 4, voff2, so, 0, 0);
             }
         };
-        // prologue: the items of planes 0 .. PDP - 1
-        for (int pi = 0; pi < PDP; ++pi) fu_static_for<RB>([&](auto Kc) { dma(pi, Kc); });
+        for (int pi = 0; pi < PDP; ++pi) dma(pi);              // prologue: planes 0 .. PDP - 1
         for (int pi = 0; pi < np; ++pi) {
             const unsigned short* const base = reinterpret_cast<const unsigned short*>(slots(pi));
             const unsigned yp = (unsigned)pi * oplane;
-            fu_static_for<RB>([&](auto Kc) {
-                constexpr int k = decltype(Kc)::value;
-                dma(pi + PDP, Kc);
-                // item t = (pi, k)'s two pieces are done once at most the operations issued
-                // after them are outstanding (vmcnt counts loads, stores and LDS-DMA together,
-                // in issue order): the 4 pieces of each of the RB * PDP items after it and the
-                // NJ stores of each loop step since -- 4 RB PDP + NJ min(t, RB PDP)
-                constexpr int NPC = 4 * RB * PDP, NST = NJ * RB * PDP;
-                static_assert(NPC + NST < 64, "vmcnt");
+            dma(pi + PDP);
+            {
+                // plane pi's 2 NR pieces are done once at most the operations issued after
+                // them are outstanding (vmcnt counts loads, stores and LDS-DMA together, in
+                // issue order): the pieces of the PDP planes after it and the RB NJ stores of
+                // each plane since -- 2 NR PDP + RB NJ min(pi, PDP)
+                constexpr int NPC = 2 * NR * PDP, NST = RB * NJ;
+                static_assert(NPC + PDP * NST < 64, "vmcnt");
                 auto wait = [](auto Nc) {
                     constexpr int N = decltype(Nc)::value;
                     __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf) | ((N >> 4) << 14));
                 };
                 if (pi >= PDP) {
-                    wait(std::integral_constant<int, NPC + NST>{});
+                    wait(std::integral_constant<int, NPC + PDP * NST>{});
                 } else {
                     fu_static_for<PDP>([&](auto Pc) {
                         constexpr int P_ = decltype(Pc)::value;
-                        if (pi == P_) wait(std::integral_constant<int, NPC + NJ * (P_ * RB + k)>{});
+                        if (pi == P_) wait(std::integral_constant<int, NPC + P_ * NST>{});
                     });
                 }
+            }
+            fu_static_for<RB>([&](auto Kc) {
+                constexpr int k = decltype(Kc)::value;
                 asm volatile("" ::: "memory");                    // LDS reads after the wait
-                const unsigned short* const s0 = base + 2 * k * RW;
+                const unsigned short* const s0 = base + (SEP ? 2 * k : r0[k] - rlo) * RW;
                 const unsigned short* const s1 = s0 + RW;
                 float v[K];
 #pragma unroll
@@ -320,6 +332,18 @@ static bool tsk_rows_ok(const Geom& g, double* qmin, double* qmax) {
     return true;
 }
 
+// Do the RB output rows of every band read at most NR input rows (i_n(a) .. i_n(a') + 1 for
+// the band's first / last row a, a'; i_n is monotone in a)?  O(h1).
+static bool tsk_bands_ok(const Geom& g, int RB, int NR) {
+    const double ch = (double)(g.h - 1) * 0.5;
+    for (int64_t a0 = 0; a0 < g.h1; a0 += RB) {
+        const int64_t a1 = std::min<int64_t>(a0 + RB, g.h1) - 1;
+        const int64_t i0 = (int64_t)(axis_at(g.xs, a0) + ch), i1 = (int64_t)(axis_at(g.xs, a1) + ch);
+        if (i1 - i0 + 2 > NR) return false;
+    }
+    return true;
+}
+
 static bool tsk_lattice_ok(const Geom& g, int nout, int wc, int al, double qmin, double qmax) {
     const double cw = ((double)g.w - 0.5) * 0.5;
     const int64_t nwin = (g.w1 + nout - 1) / nout;
@@ -333,7 +357,7 @@ static bool tsk_lattice_ok(const Geom& g, int nout, int wc, int al, double qmin,
     return true;
 }
 
-template <typename Tin, typename Tout, int K, int DB, int P>
+template <typename Tin, typename Tout, int K, int DB, int P, bool SEP>
 static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st) {
     // resident waves: 256 CUs x 4 SIMDs x 4 waves; units split into plane chunks until
     // there are >= upw units per resident wave (the records are then recomputed per chunk:
@@ -355,7 +379,7 @@ static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st)
     D.units = tiles * D.nchunk;
     const int64_t waves = std::min<int64_t>(D.units, RESIDENT);
     const unsigned blocks = (unsigned)((waves + 3) / 4);
-    hipLaunchKernelGGL((k_hexresize_down<Tin, Tout, K, DB, P>), dim3(blocks), dim3(HD_THREADS), 0, st,
+    hipLaunchKernelGGL((k_hexresize_down<Tin, Tout, K, DB, P, SEP>), dim3(blocks), dim3(HD_THREADS), 0, st,
                        (const Tin*)src, (Tout*)dst, D);
     return launch_status();
 }
@@ -389,6 +413,8 @@ int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t 
     HexDownGeom D = {};
     double qmax;
     if (!tsk_rows_ok(g, &D.qmin, &qmax)) return HG_EUNSUP;
+    const int RB = DB == 16 ? TsCfg<16>::RB : TsCfg<4>::RB, NR = DB == 16 ? TsCfg<16>::NR : TsCfg<4>::NR;
+    const bool sep = !tsk_bands_ok(g, RB, NR);       // rows shared by no two output rows
     // output windows of whole 128-B lines when the lattice allows (64 16-bit or 32 fp32
     // columns: partial lines shared by two waves cost ~10-20 %, measured), else the widest
     int nout = std::min(256, (int)std::floor((wc - 6) / std::max(ratio, 1e-3)));
@@ -409,14 +435,16 @@ int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t 
     D.h = (int)h; D.w = (int)w; D.h1 = (int)h1; D.w1 = (int)w1;
     D.nout = nout;
     D.nwin = (int)((w1 + nout - 1) / nout);
-    D.nband = (int)((h1 + (DB == 16 ? TsCfg<16>::RB : TsCfg<4>::RB) - 1) /
-                    (DB == 16 ? TsCfg<16>::RB : TsCfg<4>::RB));
+    D.nband = (int)((h1 + RB - 1) / RB);
     if (dry) return HG_OK;
+#define HG_TSK2(TI, TO, S)                                                                     \
+    if (DB == 4) return K == 4 ? hd_launch<TI, TO, 4, 4, HD_P4, S>(src, dst, D, st)            \
+                               : hd_launch<TI, TO, HD_P4, 4, HD_P4, S>(src, dst, D, st);       \
+    return K == 4 ? hd_launch<TI, TO, 4, 16, HD_P16, S>(src, dst, D, st)                        \
+                  : hd_launch<TI, TO, HD_P16, 16, HD_P16, S>(src, dst, D, st);
 #define HG_TSK(TI, TO)                                                                         \
-    if (DB == 4) return K == 4 ? hd_launch<TI, TO, 4, 4, HD_P4>(src, dst, D, st)               \
-                               : hd_launch<TI, TO, HD_P4, 4, HD_P4>(src, dst, D, st);          \
-    return K == 4 ? hd_launch<TI, TO, 4, 16, HD_P16>(src, dst, D, st)                           \
-                  : hd_launch<TI, TO, HD_P16, 16, HD_P16>(src, dst, D, st);
+    if (sep) { HG_TSK2(TI, TO, true) }                                                         \
+    HG_TSK2(TI, TO, false)
     if (sdt == HG_BF16) {
         if (ddt == HG_BF16) { HG_TSK(__bf16, __bf16) }
         if (ddt == HG_F16) { HG_TSK(__bf16, _Float16) }
@@ -426,6 +454,7 @@ int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t 
     if (ddt == HG_F16) { HG_TSK(_Float16, _Float16) }
     HG_TSK(_Float16, float)
 #undef HG_TSK
+#undef HG_TSK2
 }
 
 }  // namespace hg

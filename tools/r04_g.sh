@@ -10,7 +10,7 @@ tail -5 $OUT/pytest.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python tools/ab_ops.py wide 8 base base%HYGRID_CONV_DMA=0 2>&1 | grep -v amdgpu.ids | tee $OUT/ab_wide.txt
 for op in hr0 hr1 hr2 up; do
-  timeout -k 10 200 python tools/ab_ops.py $op 8 base i0 base%HYGRID_DOWN=0 >> $OUT/ab_ops.txt 2>&1 || exit 1
+  timeout -k 10 200 python tools/ab_ops.py $op 8 base u2 i0 base%HYGRID_DOWN=0 >> $OUT/ab_ops.txt 2>&1 || exit 1
 done
 grep -v amdgpu.ids $OUT/ab_ops.txt
 timeout -k 10 200 python tools/ab_ops.py rt 8 rtv0 rtpd4 rtpd2 2>&1 | grep -v amdgpu.ids | tee $OUT/ab_rt.txt
