@@ -25,7 +25,7 @@ from ._digest import kernel_source_digest  # noqa: E402  (re-exported)
 HG_U8, HG_I8, HG_U16, HG_I16, HG_I32, HG_I64, HG_F16, HG_BF16, HG_F32, HG_F64 = range(10)
 HG_NEAREST, HG_LINEAR = 0, 1
 HG_OP_RECT_TO_HEX, HG_OP_HEX_TO_RECT, HG_OP_HEXRESIZE = 0, 1, 2
-HG_KERNEL_GENERAL, HG_KERNEL_NEAREST, HG_KERNEL_STREAM, HG_KERNEL_DOWN = range(4)
+HG_KERNEL_GENERAL, HG_KERNEL_NEAREST, HG_KERNEL_STREAM, HG_KERNEL_DOWN, HG_KERNEL_UP = range(5)
 HG_PYR_FUSED, HG_PYR_FUSED_SHORT, HG_PYR_STREAM, HG_PYR_LDS = range(4)
 HG_OK, HG_EINVAL, HG_EDTYPE, HG_ESHAPE, HG_EUNSUP, HG_EOVERFLOW = 0, -1, -2, -3, -4, -5
 PAD_MODES = {"constant": 0, "zeros": 0, "reflect": 1, "replicate": 2, "circular": 3}

@@ -489,6 +489,10 @@ static int resample(const void* src, void* dst, int sdt, int ddt, int64_t planes
         const int rc = down_try(src, dst, sdt, ddt, planes, h, w, h1, w1, interp, s);
         if (rc != HG_EUNSUP) return rc;
     }
+    if (OP != OP_R2H && interp == HG_NEAREST) {   // upsampling lattices (ConvertToHexagon^-1)
+        const int rc = triup_try(OP, src, dst, sdt, ddt, planes, h, w, h1, w1, interp, s, false);
+        if (rc != HG_EUNSUP) return rc;
+    }
     if (interp == HG_NEAREST) {
         if (sdt != ddt) return HG_EDTYPE;
         switch (dtype_size(sdt)) {
@@ -506,7 +510,11 @@ static int resample(const void* src, void* dst, int sdt, int ddt, int64_t planes
         const int rc = stream_try(OP, src, dst, sdt, ddt, planes, h, w, h1, w1, s);
         if (rc != HG_EUNSUP) return rc;
     }
-    if (!dbl && OP != OP_R2H) {      // ~2x hexresize (pyramid levels), 2x up hex -> rect
+    if (!dbl && OP != OP_R2H) {      // upsampling lattices: hex (h/2, w/2) -> rect (h, w)
+        const int rc = triup_try(OP, src, dst, sdt, ddt, planes, h, w, h1, w1, interp, s, false);
+        if (rc != HG_EUNSUP) return rc;
+    }
+    if (!dbl && OP != OP_R2H) {      // ~2x hexresize (pyramid levels)
         const int rc = tristream_try(OP, src, dst, sdt, ddt, planes, h, w, h1, w1, s, false);
         if (rc != HG_EUNSUP) return rc;
     }
@@ -552,10 +560,16 @@ int hg_resample_kernel(int op, int sdt, int ddt, int64_t planes, int64_t h, int6
     if (op == HG_OP_RECT_TO_HEX && !dbl &&
         hg::down_try(nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, interp, nullptr, true) == HG_OK)
         return HG_KERNEL_DOWN;
+    if (interp == HG_NEAREST && op != HG_OP_RECT_TO_HEX &&
+        hg::triup_try(op, nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, interp, nullptr, true) == HG_OK)
+        return HG_KERNEL_UP;
     if (interp == HG_NEAREST) return HG_KERNEL_NEAREST;
     if (!dbl && op != HG_OP_HEXRESIZE &&
         hg::stream_try(op, nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, nullptr, true) == HG_OK)
         return HG_KERNEL_STREAM;
+    if (!dbl && op != HG_OP_RECT_TO_HEX &&
+        hg::triup_try(op, nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, interp, nullptr, true) == HG_OK)
+        return HG_KERNEL_UP;
     if (!dbl && op != HG_OP_RECT_TO_HEX && interp == HG_LINEAR &&
         hg::tristream_try(op, nullptr, nullptr, sdt, ddt, planes, h, w, h1, w1, nullptr, true) == HG_OK)
         return HG_KERNEL_DOWN;

@@ -20,6 +20,11 @@ int stream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t pla
 // window (~2x hexresize: the pyramid levels; hex (h/2, w/2) -> rect (h, w)); HG_EUNSUP otherwise
 int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h,
                   int64_t w, int64_t h1, int64_t w1, hipStream_t st, bool dry);
+// tri_up.hip: upsampling triangle resamples (op HG_OP_HEX_TO_RECT / HG_OP_HEXRESIZE whose output
+// steps are <= one input sample: the inverse of ConvertToHexagon's lattice), 'linear' on 16/32-bit
+// floats with fp32 accumulation and 'nearest' on 8/16/32-bit elements; HG_EUNSUP otherwise
+int triup_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h,
+              int64_t w, int64_t h1, int64_t w1, int interp, hipStream_t st, bool dry);
 int down_try(const void* src, void* dst, int sdt, int ddt, int64_t planes, int64_t h, int64_t w,
              int64_t h1, int64_t w1, int interp, hipStream_t st, bool dry = false);
 

@@ -110,10 +110,11 @@ int hg_resample_backward(int op, const void* gy, void* dx, int acc_dtype, int64_
  * (nothing is launched): HG_KERNEL_GENERAL (k_resample_lds / k_resample_direct),
  * HG_KERNEL_NEAREST (k_resample_nearest), HG_KERNEL_STREAM (near-identity row streaming,
  * resample_stream.hip), HG_KERNEL_DOWN (~2x downsampling streaming kernels: rect->hex,
- * resample_down.hip; hexresize (pyramid levels), hexresize_down.hip), or a
+ * resample_down.hip; hexresize (pyramid levels), hexresize_down.hip), HG_KERNEL_UP
+ * (upsampling triangle lattices, linear and nearest: hex (h/2, w/2) -> rect (h, w), tri_up.hip), or a
  * negative status.  Introspection for tests and tools; the reference has no counterpart. */
 enum hg_kernel { HG_KERNEL_GENERAL = 0, HG_KERNEL_NEAREST = 1, HG_KERNEL_STREAM = 2,
-                 HG_KERNEL_DOWN = 3 };
+                 HG_KERNEL_DOWN = 3, HG_KERNEL_UP = 4 };
 int hg_resample_kernel(int op, int src_dtype, int dst_dtype, int64_t planes, int64_t h, int64_t w,
                        int64_t h1, int64_t w1, int interp);
 

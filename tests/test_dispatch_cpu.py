@@ -62,13 +62,37 @@ def test_same_size_keeps_its_kernels():
                        _abi.HG_LINEAR) == _abi.HG_KERNEL_DOWN
     assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 2160, 3840, 68, 120,
                    _abi.HG_LINEAR) == _abi.HG_KERNEL_GENERAL
-    # hex (h/2, w/2) -> rect (h, w), the inverse of ConvertToHexagon's lattice: the same
-    # streaming triangle kernel (two output columns per lane); fp64 out keeps the general one
-    for h, w in ((2160, 3840), (540, 964), (1080, 1920)):
+    # hex (h/2, w/2) -> rect (h, w), the inverse of ConvertToHexagon's lattice: the upsampling
+    # triangle kernel (tri_up.hip), linear and nearest; HYGRID_UP=0 falls back to the
+    # downsampling triangle kernel (linear) / the general nearest kernel; fp64 out keeps the
+    # general one
+    for h, w in ((2160, 3840), (540, 964), (1080, 1920), (10, 20)):
+        for dt, ot in ((_abi.HG_BF16, _abi.HG_BF16), (_abi.HG_F16, _abi.HG_F32),
+                       (_abi.HG_F32, _abi.HG_BF16)):
+            assert _kernel(_abi.HG_OP_HEX_TO_RECT, dt, ot, 96, h // 2, w // 2, h, w,
+                           _abi.HG_LINEAR) == _abi.HG_KERNEL_UP
         assert _kernel(_abi.HG_OP_HEX_TO_RECT, _abi.HG_BF16, _abi.HG_BF16, 96, h // 2, w // 2, h,
-                       w, _abi.HG_LINEAR) == _abi.HG_KERNEL_DOWN
+                       w, _abi.HG_LINEAR, HYGRID_UP="0") in (_abi.HG_KERNEL_DOWN, _abi.HG_KERNEL_GENERAL)
         assert _kernel(_abi.HG_OP_HEX_TO_RECT, _abi.HG_BF16, _abi.HG_F64, 96, h // 2, w // 2, h,
                        w, _abi.HG_LINEAR) == _abi.HG_KERNEL_GENERAL
+        for dt in (_abi.HG_U8, _abi.HG_BF16, _abi.HG_I32):
+            if (w // 2) * {_abi.HG_U8: 1, _abi.HG_BF16: 2, _abi.HG_I32: 4}[dt] % 4:
+                continue     # input rows not dword-aligned for LDS-DMA
+            assert _kernel(_abi.HG_OP_HEX_TO_RECT, dt, dt, 96, h // 2, w // 2, h, w,
+                           _abi.HG_NEAREST) == _abi.HG_KERNEL_UP
+            assert _kernel(_abi.HG_OP_HEX_TO_RECT, dt, dt, 96, h // 2, w // 2, h, w,
+                           _abi.HG_NEAREST, HYGRID_UP="0") == _abi.HG_KERNEL_NEAREST
+    # an output width no K divides: one column per lane
+    assert _kernel(_abi.HG_OP_HEX_TO_RECT, _abi.HG_BF16, _abi.HG_BF16, 3, 5, 10, 10, 19,
+                   _abi.HG_LINEAR) == _abi.HG_KERNEL_UP
+    # hexresize upsampling takes it too; downsampling never does
+    assert _kernel(_abi.HG_OP_HEXRESIZE, _abi.HG_F16, _abi.HG_F16, 3, 540, 960, 1080, 1920,
+                   _abi.HG_LINEAR) == _abi.HG_KERNEL_UP
+    assert _kernel(_abi.HG_OP_HEX_TO_RECT, _abi.HG_U8, _abi.HG_U8, 3, 1080, 1920, 540, 960,
+                   _abi.HG_NEAREST) == _abi.HG_KERNEL_NEAREST
+    # odd input widths: rows not dword-aligned for 16-bit LDS-DMA
+    assert _kernel(_abi.HG_OP_HEX_TO_RECT, _abi.HG_BF16, _abi.HG_BF16, 3, 33, 125, 66, 250,
+                   _abi.HG_LINEAR) != _abi.HG_KERNEL_UP
 
 
 def test_outside_the_domain():

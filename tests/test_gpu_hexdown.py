@@ -184,7 +184,7 @@ def test_h2r_2x_up_bit_identical_and_vs_oracle(shape, pair):
     B, C = x.shape[:2]
     k = _abi.resample_kernel(_abi.HG_OP_HEX_TO_RECT, _abi.dtype_code(dt), _abi.dtype_code(od),
                              B * C, h, w, h1, w1)
-    assert k == _abi.HG_KERNEL_DOWN
+    assert k == _abi.HG_KERNEL_UP        # the upsampling kernel (tests/test_gpu_triup.py)
     y = ops.hex_to_rect(x, (h1, w1), out_dtype=od)
     torch.cuda.synchronize()
     _same_bits(y, _general(ops.hex_to_rect, x, (h1, w1), out_dtype=od))

@@ -55,13 +55,19 @@ def main():
         B, C, H, W, t = 8, 3, 1080, 1920, torch.float16
     elif op == "up":
         B, C, H, W, t = 32, 3, 1080, 1920, torch.bfloat16
+    elif op == "upn":
+        B, C, H, W, t = 32, 3, 1080, 1920, torch.uint8
     else:
         B, C, H, W, t = 8, 3, 4320, 7680, torch.float16
-    x = torch.rand((B, C, H, W), generator=g, device=dev, dtype=t)
+    if t == torch.uint8:
+        x = torch.randint(0, 256, (B, C, H, W), generator=g, device=dev, dtype=t)
+        dt[t] = _abi.HG_U8
+    else:
+        x = torch.rand((B, C, H, W), generator=g, device=dev, dtype=t)
     taps = (torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32, device=dev) / 12).repeat(C)
     if op.startswith("pyr") or op.startswith("hr"):
         y = torch.empty((B, C, H // 2, W // 2), device=dev, dtype=t)
-    elif op == "up":
+    elif op in ("up", "upn"):
         y = torch.empty((B, C, 2 * H, 2 * W), device=dev, dtype=t)
     else:
         y = torch.empty_like(x)
@@ -87,10 +93,11 @@ def main():
             f = lib.hg_hexresize
             f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_int, _vp]
             return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, H // 2, W // 2, 1, s)
-        if op == "up":
+        if op in ("up", "upn"):
             f = lib.hg_hex_to_rect
             f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_int, _vp]
-            return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, 2 * H, 2 * W, 1, s)
+            return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, 2 * H, 2 * W,
+                     0 if op == "upn" else 1, s)
         if op in ("conv", "wide"):
             f = lib.hg_hexconv2d
             f.argtypes = [_vp] * 4 + [_int] * 3 + [_i64] * 5 + [_int] * 7 + [_dbl, _vp]

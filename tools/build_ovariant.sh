@@ -11,7 +11,7 @@ SRC=$1; NAME=$2; shift 2
 OBJ=$PKG/build/obj
 OUT=$PKG/HyGrid/_lib/variants
 mkdir -p "$OUT" "$OBJ/variants"
-OBJS=${OBJS:-"abi resample resample_stream resample_down hexresize_down"}
+OBJS=${OBJS:-"abi resample resample_stream resample_down hexresize_down tri_up"}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "$@" \
     -I"$PKG/csrc" -c "$PKG/csrc/$SRC.hip" -o "$OBJ/variants/${SRC}_$NAME.o"
 LINK=""

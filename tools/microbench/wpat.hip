@@ -1,0 +1,170 @@
+// Microbenchmark (round 4): write patterns of the upsampling triangle kernel (tri_up.hip) at
+// the inverse-lattice line's output (32 x 3 planes of 2160 x 3840 bf16 = 1.59 GB), stores
+// only, no loads or arithmetic: which (unit shape, store width, walk order) can the HBM absorb
+// at fill_'s rate (6.8 TB/s)?
+//   unit = (window of 64 * SB / 2 columns, band of RB rows, all 96 planes); a wave stores, per
+//   plane, its RB rows as one SB-byte store per lane each; PO = 1: planes outer (the kernel
+//   today: plane, then row), PO = 0: rows outer (row, then plane).
+//   WALK = 1: unit = (window, plane) walking a band of RB rows (the row-streaming kernels'
+//   order: consecutive stores of a wave are consecutive rows of one plane)
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+#include <type_traits>
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+constexpr int H = 2160, W = 3840, P = 96;
+template <int N> using IC = std::integral_constant<int, N>;
+template <int N, int I = 0, typename F> __device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (I < N) { f(IC<I>{}); sfor<N, I + 1>(f); }
+}
+
+__device__ __forceinline__ unsigned xcd_swz(unsigned bid, unsigned nwg) {
+    const unsigned q = nwg >> 3, r = nwg & 7u, x = bid & 7u;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+template <int SB, int RB, int PO, int WALK, int LM = 0, int PD = (LM == 0 ? 1 : (LM == 1 ? 2 : 1) * (RB / 2 + 2) + RB > 10 ? 63 / ((LM == 1 ? 2 : 1) * (RB / 2 + 2) + RB) : 6)>
+__global__ __launch_bounds__(256) void wpat(uint16_t* __restrict__ y, const uint16_t* __restrict__ x, int nunits) {
+    // LM 1: per plane, 3 input rows of a (1080 x 1920) bf16 plane by LDS-DMA (256 B from all
+    // lanes + 32 B from lanes 0-7 per row, the kernel's pattern) into a per-wave ring, waited
+    // PD planes later with a counted vmcnt; LM 2: the same rows as dword loads into VGPRs
+    constexpr int NRR = RB / 2 + 2;   // input rows per band (2x upsampling)
+    __shared__ __attribute__((aligned(16))) unsigned char ring_all[4][LM ? (PD + 1) * NRR * 304 : 16];
+    unsigned char* const ring = ring_all[threadIdx.x >> 6];
+    unsigned vacc = 0;
+    unsigned vr[PD + 1][NRR];
+    constexpr int COLS = 64 * SB / 2;
+    constexpr int NWIN = W / COLS, NB = (H + RB - 1) / RB;
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    const int64_t wid = (int64_t)xcd_swz(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+    typedef unsigned u2 __attribute__((ext_vector_type(2)));
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    for (int64_t u = wid; u < nunits; u += nwaves) {
+        const int win = (int)(u % NWIN);
+        const int64_t r_ = u / NWIN;
+        int band, p0, np;
+        if (WALK) { band = (int)(r_ % NB); p0 = (int)(r_ / NB); np = 1; }
+        else { band = (int)r_; p0 = 0; np = P; }
+        const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(y + (int64_t)p0 * H * W), (short)0, (int)std::min<int64_t>((int64_t)np * H * W * 2, 0x7fffffff), 0x00020000);
+        const unsigned vo = (unsigned)(win * COLS + lane * (SB / 2)) * 2u;
+        const int a0 = band * RB;
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)x, (short)0, 0x7fffffff, 0x00020000);
+        const unsigned xo0 = (unsigned)(win * (COLS / 2) + 2 * lane) * 2u, xo1 = xo0 + 256;
+        const unsigned xo16 = (unsigned)(win * (COLS / 2) + 8 * lane) * 2u;
+        auto ld = [&](int p, auto SLc) {
+            constexpr int SL = decltype(SLc)::value;
+            if constexpr (LM == 0) return;
+#pragma unroll
+            for (int q = 0; q < NRR; ++q) {
+                const unsigned so = (unsigned)(p % 96) * (1080u * 1920u * 2u) + (unsigned)min(a0 / 2 + q, 1079) * 3840u;
+                if constexpr (LM == 3) {   // one 16-B piece per lane, lanes 0-17 (288 B)
+                    auto* l0 = (__attribute__((address_space(3))) void*)(ring + (SL * NRR + q) * 304);
+                    if (lane < 18) __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, l0, 16, xo16, so, 0, 0);
+                } else if constexpr (LM == 1) {
+                    auto* l0 = (__attribute__((address_space(3))) void*)(ring + (SL * NRR + q) * 304);
+                    auto* l1 = (__attribute__((address_space(3))) void*)(ring + (SL * NRR + q) * 304 + 256);
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, l0, 4, xo0, so, 0, 0);
+                    if (lane < 8) __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, l1, 4, xo1, so, 0, 0);
+                } else {
+                    vr[SL][q] = __builtin_amdgcn_raw_buffer_load_b32(xr, xo0, so, 0);
+                }
+            }
+        };
+        auto wt = [&](auto SLc) {
+            constexpr int SL = decltype(SLc)::value;
+            if constexpr (LM == 0) return;
+            constexpr int N = PD * ((LM == 1 ? 2 : 1) * NRR + RB);
+            static_assert(N < 64, "vmcnt");
+            __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf) | ((N >> 4) << 14));
+            if constexpr (LM == 1) vacc += *reinterpret_cast<const unsigned*>(ring + SL * NRR * 304 + 4 * lane);
+            else vacc += vr[SL][0] + vr[SL][1];
+        };
+        auto st = [&](int p, int a) {
+            const unsigned so = (unsigned)p * (H * W * 2u) + (unsigned)min(a, H - 1) * (W * 2u);
+            if constexpr (SB == 4) __builtin_amdgcn_raw_buffer_store_b32((unsigned)(p + a), yr, vo, so, 0);
+            else if constexpr (SB == 8) __builtin_amdgcn_raw_buffer_store_b64(u2{(unsigned)p, (unsigned)a}, yr, vo, so, 0);
+            else __builtin_amdgcn_raw_buffer_store_b128(u4{(unsigned)p, (unsigned)a, 1u, 2u}, yr, vo, so, 0);
+        };
+        if (LM) {
+            sfor<PD>([&](auto Ic) { ld(decltype(Ic)::value, Ic); });
+            auto body = [&](int p, auto SLc) {
+                constexpr int SL = decltype(SLc)::value;
+                ld(p + PD, IC<(SL + PD) % (PD + 1)>{});
+                wt(SLc);
+#pragma unroll
+                for (int k = 0; k < RB; ++k) st(p, a0 + k);
+            };
+            int p = 0;
+            for (; p + PD + 1 <= np; p += PD + 1) sfor<PD + 1>([&](auto Sc) { body(p + decltype(Sc)::value, Sc); });
+            sfor<PD>([&](auto Sc) { if (p + decltype(Sc)::value < np) body(p + decltype(Sc)::value, Sc); });
+            __builtin_amdgcn_s_waitcnt(0x0f70);
+        } else if (PO) {
+            for (int p = 0; p < np; ++p)
+#pragma unroll
+                for (int k = 0; k < RB; ++k) st(p, a0 + k);
+        } else {
+#pragma unroll 2
+            for (int k = 0; k < RB; ++k)
+                for (int p = 0; p < np; ++p) st(p, a0 + k);
+        }
+    }
+    if (vacc == 0x12345678u) y[0] = 1;
+}
+
+template <typename K>
+float timeit(K k, int reps) {
+    hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) k();
+    CK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int i = 0; i < reps; ++i) {
+        CK(hipEventRecord(e0)); k(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+static const double GB = 2.0 * P * H * W / 1e9;
+template <int SB, int RB, int PO, int WALK, int LM = 0>
+void run(const char* what, uint16_t* y, int waves_cap, const uint16_t* x = nullptr) {
+    constexpr int COLS = 64 * SB / 2;
+    constexpr int NWIN = W / COLS, NB = (H + RB - 1) / RB;
+    const int nunits = WALK ? NWIN * NB * P : NWIN * NB;
+    const int waves = std::min(nunits, waves_cap);
+    const float ms = timeit([&] { hipLaunchKernelGGL((wpat<SB, RB, PO, WALK, LM>), dim3((waves + 3) / 4), dim3(256), 0, 0, y, x, nunits); }, 9);
+    printf("%-40s store %2d B/lane  RB %4d  %s: units %7d  %.4f ms  %.3f of 8 TB/s\n", what, SB, RB,
+           PO ? "plane-outer" : "row-outer  ", nunits, ms, GB / ms * 1e3 / 8000);
+    fflush(stdout);
+}
+
+int main() {
+    const size_t n = (size_t)P * H * W;
+    uint16_t* y;
+    CK(hipMalloc(&y, n * 2));
+    CK(hipMemset(y, 0, n * 2));
+    const float mf = timeit([&] { CK(hipMemsetAsync(y, 1, n * 2, 0)); }, 9);
+    printf("%-40s %.4f ms  %.3f of 8 TB/s\n", "hipMemset (ceiling)", mf, GB / mf * 1e3 / 8000);
+    const int R = 16384;
+    uint16_t* x;
+    CK(hipMalloc(&x, (size_t)96 * 1080 * 1920 * 2));
+    CK(hipMemset(x, 0, (size_t)96 * 1080 * 1920 * 2));
+    for (int rep = 0; rep < 2; ++rep) {
+        run<8, 2, 1, 0>("tri_up today (stores only)", y, R);
+        run<16, 2, 1, 0>("16-B stores", y, R);
+        run<8, 2, 1, 0, 1>("+ LDS-DMA rows (tri_up's memory side)", y, R, x);
+        run<8, 2, 1, 0, 2>("+ VGPR dword rows", y, R, x);
+        run<16, 2, 1, 0, 1>("16-B stores + LDS-DMA rows", y, R, x);
+        run<8, 4, 1, 0, 1>("RB 4 + LDS-DMA rows (4 per plane)", y, R, x);
+        run<8, 4, 1, 0, 2>("RB 4 + VGPR rows", y, R, x);
+        run<16, 4, 1, 0, 1>("RB 4, 16-B stores + LDS-DMA rows", y, R, x);
+        run<8, 8, 1, 0, 2>("RB 8 + VGPR rows", y, R, x);
+    }
+    return 0;
+}
