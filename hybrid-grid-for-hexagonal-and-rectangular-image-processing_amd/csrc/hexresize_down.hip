@@ -54,7 +54,7 @@ __device__ __forceinline__ void fu_static_for(F&& f) {
 #define HD_PDP16 1          // 16-B pieces: planes in flight ahead of the one blended
 #endif
 #ifndef HD_RB4
-#define HD_RB4 4
+#define HD_RB4 2            // (4 spilled 277 VGPRs: r04 ISA; up-lattices now run tri_up.hip)
 #endif
 #ifndef HD_NR16
 #define HD_NR16 4           // 16-B pieces: input rows loaded per (unit, plane) (host-checked)
@@ -166,6 +166,8 @@ __global__ __launch_bounds__(HD_THREADS, HD_WPE) void k_hexresize_down(const Tin
             const int a = a0 + min(k, nr - 1);
 #pragma unroll
             for (int kk = 0; kk < K; ++kk) {
+                // one sample's fp64 temporaries at a time (interleaved samples spill)
+                __builtin_amdgcn_sched_barrier(0);
                 const int bb = b0 + P * lane + 64 * P * (kk / P) + kk % P;
                 const TriSample s = tri_sample(D.g, a, bb < bend ? bb : b0);
                 if (kk == 0) r0[k] = __builtin_amdgcn_readfirstlane((int)s.i_n);   // i_n: row only
@@ -179,6 +181,7 @@ __global__ __launch_bounds__(HD_THREADS, HD_WPE) void k_hexresize_down(const Tin
             }
             yo[k] = (unsigned)a * orow;
         }
+        __builtin_amdgcn_sched_barrier(0);
         // per store j: the lane's byte offset in the row when all its P columns are in the
         // window; else lane 0 (whose column b0 always is, and b0 + 1 for P = 2: host) repeats
         // store 0, so no store has all its lanes out of range; a lane with only its first

@@ -8,6 +8,7 @@ usage: python tools/prof_ops.py OP [iters]
   hr0  hexresize 8K -> 4K fp16 b8 (the pyramid chain's level-0 hexresize); hr1 4K -> 2K,
        hr2 2K -> 1K (levels 1, 2)
   up   hex (1080, 1920) -> rect (2160, 3840) bf16 b32
+  wide HexConv2d(64, 64, 0, 2, padding=1) bf16, 4 x 64 x 1080 x 1920 (the bench's wide line)
 """
 import os
 import sys
@@ -42,6 +43,13 @@ def main():
     elif op == "up":
         x = torch.rand((32, 3, 1080, 1920), device=dev, dtype=torch.bfloat16)
         fn = lambda: ops.hex_to_rect(x, (2160, 3840))  # noqa: E731
+    elif op == "wide":
+        from HyGrid.HexFrames import HexConv2d
+        x = (torch.rand((4, 64, 1080, 1920), device=dev) - 0.5).to(torch.bfloat16)
+        torch.manual_seed(5)
+        conv = HexConv2d(64, 64, 0, 2, padding=1, bias=True).to(dev)
+        conv.out_dtype = torch.bfloat16
+        fn = lambda: conv(x)  # noqa: E731
     else:
         raise SystemExit(f"unknown op {op}")
     with torch.no_grad():
