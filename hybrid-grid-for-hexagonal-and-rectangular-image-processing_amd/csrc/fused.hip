@@ -117,6 +117,10 @@ int fused_rt_try(const void* x, void* y, int x_dtype, int y_dtype, int64_t plane
     return HG_EUNSUP;
 }
 
+// fused4.hip: the 4-column variant of MD 0 (bf16, C = O = 3), or HG_EUNSUP
+int fused4_try(const void* x, const float* k, const float* bias, void* y, int x_dtype, int y_dtype,
+               int C, int O, int G, const FusedGeom& F0, int op, hipStream_t st);
+
 int fused_try(const void* x, const float* kernel, const float* bias, void* y, int x_dtype,
               int y_dtype, int64_t batch, int C, int O, int G, int64_t h, int64_t w,
               int64_t h1, int64_t w1, int64_t h2, int64_t w2, int padding, int op,
@@ -138,6 +142,10 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
     F.rys = g.ys;
     F.nwin = (int)((w2 + FU_OWN - 1) / FU_OWN);
     F.nband = (int)((h2 + fu_rb(0) - 1) / fu_rb(0));
+    {
+        const int rc4 = fused4_try(x, kernel, bias, y, x_dtype, y_dtype, C, O, G, F, op, st);
+        if (rc4 != HG_EUNSUP) return rc4;
+    }
 #if FU_MIN_INST == 2   // debugging variants: fp32 C = O = 1 only
     if (x_dtype == HG_F32 && y_dtype == HG_F32 && C == 1 && O == 1 && G == 1)
         return fused_launch<float, float, 1, 1, 1>(x, kernel, bias, y, F, op, st);
@@ -171,8 +179,17 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
 
 }  // namespace hg
 
+namespace hg { void fused4_layout(int* band_rows, int* win_own, int* win_halo); }
+
+// md 0-2: the two-column kernel's modes; md 6: MD 0's four-column variant (fused4.hip: bf16,
+// C = O = 3, widths a multiple of 4)
 extern "C" int hg_fused_layout(int md, int* band_rows, int* win_own, int* win_halo) {
-    if (md < 0 || md > 2 || !band_rows || !win_own || !win_halo) return HG_EINVAL;
+    if (!band_rows || !win_own || !win_halo) return HG_EINVAL;
+    if (md == 6) {
+        hg::fused4_layout(band_rows, win_own, win_halo);
+        return HG_OK;
+    }
+    if (md < 0 || md > 2) return HG_EINVAL;
     *band_rows = hg::fu_rb(md);
     *win_own = hg::FU_OWN;
     *win_halo = hg::FU_HL;

@@ -22,6 +22,7 @@ _i64, _int, _vp, _dbl = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_
 
 
 def load(name):
+    name = name.split("%")[0]        # name%VAR=value: the library with an A/B switch set
     path = os.path.join(LIBDIR, "libhygrid_hip.so") if name == "base" else \
         os.path.join(LIBDIR, "variants", f"libhygrid_{name}.so")
     lib = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
@@ -55,6 +56,9 @@ def main():
         rng.shuffle(order)               # no fixed position in the round (clock / heat drift)
         rt = {}
         for n, f in order:
+            env = n.split("%")[1].split("=") if "%" in n else None
+            if env:
+                os.environ[env[0]] = env[1]
             for rep in range(3):         # back-to-back launches; the last one is timed
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -62,6 +66,8 @@ def main():
                 e1.record()
                 if rc != 0:
                     raise SystemExit(f"{n}: status {rc}")
+            if env:
+                del os.environ[env[0]]
             e1.synchronize()
             rt[n] = e0.elapsed_time(e1)
             if r == rounds:
