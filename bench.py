@@ -409,10 +409,10 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": traffic_note,
                 "alg_bytes_per_launch": alg_bytes[dom],
-                "limiter": "VALU issue and memory together for the fused kernel (4 waves per "
-                           "SIMD, 120 VGPRs, ~440 issue cycles per wave-step of 63 packed "
-                           "stencil FMAs + r2h / h2r): a build whose loads and stores hit one "
-                           "cache-resident row runs 12-15 % faster (DESIGN.md section 6)"
+                "limiter": "VALU issue and memory together for the fused kernel (k_fused4: 4 "
+                           "columns per lane, 150 VGPRs, 3 waves per SIMD; 126 packed stencil "
+                           "FMAs + r2h / h2r per 240-column wave-step); the 2-column kernel's "
+                           "cache-resident build ran 12-15 % faster than it (DESIGN.md section 6)"
                 if dom == "pipeline_r2h_conv_h2r" else "hbm"}
 
     compare = None

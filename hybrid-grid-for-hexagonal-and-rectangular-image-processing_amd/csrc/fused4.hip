@@ -9,8 +9,10 @@
 // every pair, 1/16 of its work on the 8-column window halo and reads 1.107x its input bytes;
 // here the neighbours of pair A are pair B's values (no DPP), the halo is 1/32 and the reads
 // ~1.04x; 8-B loads and stores per lane (walk6: the access pattern alone 0.615 -> 0.657 of
-// 8 TB/s at 42-row bands, 0.73 at 18-24; profiles/r04/walk6_b.txt).  Cost: ~160 VGPRs, 3 waves
-// per SIMD instead of 4.
+// 8 TB/s at 42-row bands, 0.73 at 18-24; profiles/r04/walk6_b.txt).  Registers: 29 of the 32
+// weight pairs in SGPRs (102 SGPRs) and one rect row of prefetch keep it at 124 VGPRs, 4 waves
+// per SIMD (21 pairs / 2 rows ahead: 150 VGPRs, 3 waves; both 1-3 % faster than k_fused MD 0
+// in in-process A/Bs on three boxes, profiles/r04/f4/).
 //
 // Domain: fused_try's (same-size lattice, padding 1, value 0) with bf16 in and out, C = O = 3,
 // groups 1, w and w2 multiples of 4.  Results within the fp32 rounding of k_fused MD 0 (the same
@@ -24,13 +26,16 @@
 namespace hg {
 
 #ifndef F4_RB_
-#define F4_RB_ 30                      // output rows per band (multiple of 6; 42 / 36 / 24 / 18 / 60: profiles/r04/f4)
+#define F4_RB_ 42                      // output rows per band (multiple of 6; 18-60 within +-2 %: profiles/r04/f4)
 #endif
 #ifndef F4_PD
-#define F4_PD 2                        // rect rows loaded ahead of use (1..4; 3 and 4 measured slower)
+#define F4_PD 1                        // rect rows loaded ahead of use (1..4): 1 fits 124 VGPRs
+#endif
+#ifndef F4_WPS
+#define F4_WPS 29                      // weight pairs in SGPRs (the rest in VGPRs): 102 SGPRs
 #endif
 #ifndef F4_WPE
-#define F4_WPE 3                       // waves per SIMD asked of the register allocator
+#define F4_WPE 4                       // waves per SIMD asked of the register allocator
 #endif
 constexpr int F4_GW = 4, F4_THREADS = 256;
 constexpr int F4_HL = 8, F4_OWN = 240;  // window halo (left) and owned columns
@@ -153,7 +158,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     int vz = 0;
     asm volatile("" : "+v"(vz));
     constexpr int NW = O * C * 7, NWP = (NW + 1) / 2;
-    constexpr int NWS = FU_WPS < NWP ? FU_WPS : NWP;
+    constexpr int NWS = F4_WPS < NWP ? F4_WPS : NWP;
     float wk[NW];
 #pragma unroll
     for (int i = 0; i < NW; ++i) wk[i] = kern[i + (i / 2 < NWS ? 0 : vz)];
