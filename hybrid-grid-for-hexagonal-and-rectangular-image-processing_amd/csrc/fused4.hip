@@ -26,7 +26,7 @@
 namespace hg {
 
 #ifndef F4_RB_
-#define F4_RB_ 42                      // output rows per band (multiple of 6; 18-60 within +-2 %: profiles/r04/f4)
+#define F4_RB_ 30                      // output rows per band (multiple of 6; 30 the most even across boxes: profiles/r04/f4)
 #endif
 #ifndef F4_PD
 #define F4_PD 1                        // rect rows loaded ahead of use (1..4): 1 fits 124 VGPRs
