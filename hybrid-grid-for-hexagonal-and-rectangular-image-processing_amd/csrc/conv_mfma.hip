@@ -392,7 +392,11 @@ __device__ __forceinline__ void cd_wait_vm() {
     __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf) | ((N >> 4) << 14));
 }
 
-template <typename Tout, int NOT>
+// WDB: weight chunks double-buffered (the next chunk's DMA overlaps this chunk's MFMAs; 71 KB of
+// LDS -> 2 workgroups per CU) or single-buffered (the DMA of chunk i + 1 is issued once chunk i's
+// MFMAs are done and waited for at the top of the next chunk; 47 KB -> 3 workgroups per CU, whose
+// MFMAs cover each other's waits)
+template <typename Tout, int NOT, bool WDB>
 __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
                                                                    const cm_u4* __restrict__ wf,
                                                                    const int* __restrict__ flag,
@@ -406,8 +410,8 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
     constexpr int PPW = CM_CC * CM_PR / 4;                // raw P row pieces per wave (12)
     static_assert(WPC % 4 == 0, "pieces");
     // one LDS array (so the DMA's M0 bases come from it): [psb | wsb x 2 | praw x 2]
-    constexpr int LPSB = CB_PSZ * 16, LWSB = WSZ * 16, LPRAW = CD_PRAW * 4;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[LPSB + 2 * LWSB + 2 * LPRAW];
+    constexpr int LPSB = CB_PSZ * 16, LWSB = WSZ * 16, LPRAW = CD_PRAW * 4, NWB = WDB ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LPSB + NWB * LWSB + 2 * LPRAW];
     cm_u4* const psb = reinterpret_cast<cm_u4*>(lds);
     const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -456,8 +460,8 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)wf, (short)0, 0x7fffffff, 0x00020000);
 
-    auto dma = [&](int ci) {                              // chunk ci -> buffers (ci & 1)
-        const int buf = ci & 1;
+    auto dma_w = [&](int ci) {                            // chunk ci's weights -> buffer
+        const int buf = WDB ? (ci & 1) : 0;
         // weights: pieces j = wv * WPW + i of the chunk's (pt, kb) blocks of CM_O * 4 fragments
 #pragma unroll
         for (int i = 0; i < WPW; ++i) {
@@ -471,6 +475,9 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
                          "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
                          : "=&s"(keep) : "v"(vo), "s"(wr), "s"(lda), "s"(so) : "memory");
         }
+    };
+    auto dma_p = [&](int ci) {                            // chunk ci's raw P rows -> buffer (ci & 1)
+        const int buf = ci & 1;
         if (interior) {
             // P rows: pieces j = wv * PPW + i = (cc, pr); lanes 0-39 one dword each
 #pragma unroll
@@ -480,7 +487,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
                 const int c = ci * CM_CC + cc;
                 const unsigned so = c < G.C ? (unsigned)((((int64_t)c * G.h + (r0 + pr - G.p)) * G.w + xs) * 2)
                                             : 0x80000000u;
-                const unsigned lda = lds0 + LPSB + 2 * LWSB + buf * LPRAW + j * CD_PRW * 4;
+                const unsigned lda = lds0 + LPSB + NWB * LWSB + buf * LPRAW + j * CD_PRW * 4;
                 const unsigned vo = lane * 4u;
                 unsigned keep;
                 if (lane < CD_PRW)
@@ -495,20 +502,30 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
     // every wave issues the same number of DMA instructions per chunk (counted waits)
     constexpr int NW = WPW, NP_ = PPW;
 
-    dma(0);
+    dma_w(0);
+    dma_p(0);
     for (int ci = 0; ci < nch; ++ci) {
         const int buf = ci & 1;
         const int c0 = ci * CM_CC;
+        // chunk ci's pieces are done once at most the ones issued after them are outstanding
+        // (vmcnt counts them in issue order): double-buffered, W(ci+1) and P(ci+1); single,
+        // only P(ci+1) (W(ci) was issued at the end of chunk ci-1, before P(ci+1))
         if (ci + 1 < nch) {
-            dma(ci + 1);
-            if (interior) cd_wait_vm<NW + NP_>(); else cd_wait_vm<NW>();
+            if constexpr (WDB) {
+                dma_w(ci + 1);
+                dma_p(ci + 1);
+                if (interior) cd_wait_vm<NW + NP_>(); else cd_wait_vm<NW>();
+            } else {
+                dma_p(ci + 1);
+                if (interior) cd_wait_vm<NP_>(); else cd_wait_vm<0>();
+            }
         } else {
             cd_wait_vm<0>();
         }
         // ---- P chunk -> psb (channel-innermost fragments) -------------------------------
         if (interior) {
             __builtin_amdgcn_s_barrier();                 // every wave's raw rows have landed
-            const unsigned short* raw = reinterpret_cast<const unsigned short*>(lds + LPSB + 2 * LWSB + buf * LPRAW);
+            const unsigned short* raw = reinterpret_cast<const unsigned short*>(lds + LPSB + NWB * LWSB + buf * LPRAW);
             for (int f = tid; f < CM_PR * CB_PP; f += CM_THREADS) {
                 const int pr = f / CB_PP, pc = f - pr * CB_PP;
                 unsigned short v[8];
@@ -545,7 +562,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
         __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): this wave's LDS writes
         __builtin_amdgcn_s_barrier();                     // psb and the weights complete
         // ---- 2 k blocks x 4 column tiles x 3 weight parts x NOT channel tiles -------------
-        const cm_u4* const wsb = reinterpret_cast<const cm_u4*>(lds + LPSB + buf * LWSB);
+        const cm_u4* const wsb = reinterpret_cast<const cm_u4*>(lds + LPSB + (WDB ? buf : 0) * LWSB);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             cm_b8 bf[4];
@@ -566,6 +583,9 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_s_barrier();                     // psb / this buffer free again
+        if constexpr (!WDB) {
+            if (ci + 1 < nch) dma_w(ci + 1);              // the single weight buffer is free
+        }
     }
 
     if (r >= G.ho) return;
@@ -621,7 +641,8 @@ int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_
     }
     G.ntq = (G.wo + CM_Q - 1) / CM_Q;
     G.ntr = (G.ho + CM_ROWS - 1) / CM_ROWS;
-    const int nt = G.O <= 32 ? 2 : 4;                  // output-channel tiles per workgroup
+    // output-channel tiles per workgroup (A/B switch HYGRID_CONV_NT=2: two for any O)
+    const int nt = (G.O <= 32 || env_is("HYGRID_CONV_NT", "2")) ? 2 : 4;
     G.nto = (G.O + 16 * nt - 1) / (16 * nt);
     const int64_t blocks = B * (int64_t)G.ntq * G.ntr * G.nto;
     if (blocks > INT_MAX || blocks == 0) return blocks == 0 ? HG_OK : HG_EUNSUP;
@@ -643,13 +664,16 @@ int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_
             cm_u4* wfr = static_cast<cm_u4*>(ws);
             int* flg = reinterpret_cast<int*>(static_cast<char*>(ws) + wbytes);
             hipLaunchKernelGGL(k_wsplit_bf16, dim3(nch, Opad / 16), dim3(128), 0, st, k, wfr, flg, G.C, G.O, Opad);
+            // weight chunks single-buffered (A/B switch HYGRID_CONV_WDB=1: double-buffered)
+            const bool wdb = env_is("HYGRID_CONV_WDB", "1");
+#define HG_CD_LAUNCH2(TO, NT_, WDB_)                                                          \
+            hipLaunchKernelGGL((k_hexconv_mfma_bf16d<TO, NT_, WDB_>), grid, blk, 0, st, (const __bf16*)x, wfr, flg, b, (TO*)y, G, Opad);
 #define HG_CD_LAUNCH(TO)                                                                      \
-            if (nt == 2)                                                                      \
-                hipLaunchKernelGGL((k_hexconv_mfma_bf16d<TO, 2>), grid, blk, 0, st, (const __bf16*)x, wfr, flg, b, (TO*)y, G, Opad); \
-            else                                                                              \
-                hipLaunchKernelGGL((k_hexconv_mfma_bf16d<TO, 4>), grid, blk, 0, st, (const __bf16*)x, wfr, flg, b, (TO*)y, G, Opad);
+            if (nt == 2) { if (wdb) { HG_CD_LAUNCH2(TO, 2, true) } else { HG_CD_LAUNCH2(TO, 2, false) } } \
+            else { if (wdb) { HG_CD_LAUNCH2(TO, 4, true) } else { HG_CD_LAUNCH2(TO, 4, false) } }
             if (y_dtype == HG_BF16) { HG_CD_LAUNCH(__bf16) } else { HG_CD_LAUNCH(float) }
 #undef HG_CD_LAUNCH
+#undef HG_CD_LAUNCH2
             const int ls = launch_status();
             const hipError_t fe = hipFreeAsync(ws, st);
             return ls != HG_OK ? ls : (int)fe;

@@ -34,6 +34,9 @@ namespace hg {
 #ifndef F4_WPS
 #define F4_WPS 29                      // weight pairs in SGPRs (the rest in VGPRs): 102 SGPRs
 #endif
+#ifndef F4_ORDER
+#define F4_ORDER 0                     // workgroup order (A/B): 0 group fastest, 1 band fastest
+#endif
 #ifndef F4_WPE
 #define F4_WPE 4                       // waves per SIMD asked of the register allocator
 #endif
@@ -63,10 +66,11 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     float4* const lut = lut_all[wslot];
     const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
     const int ngrp = (F.nwin + F4_GW - 1) / F4_GW;
-    const int grp = (int)(blk % ngrp);
-    const int64_t rest = blk / ngrp;
-    const int band = (int)(rest % F.nband);
-    const int64_t b = rest / F.nband;
+    // block -> (window group, band, image): group fastest (F4_ORDER 0) or band fastest (1: the
+    // bands of one window group run side by side, sharing their 4 halo rows in L2)
+    const int grp = (int)(F4_ORDER ? (blk / F.nband) % ngrp : blk % ngrp);
+    const int band = (int)(F4_ORDER ? blk % F.nband : (blk / ngrp) % F.nband);
+    const int64_t b = blk / ((int64_t)ngrp * F.nband);
     if (b >= F.B) return;                            // uniform per workgroup
     const int win = grp * F4_GW + wslot;             // may be >= nwin: runs, owns nothing
     const int W0 = win * F4_OWN - F4_HL;
