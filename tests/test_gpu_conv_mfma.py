@@ -266,6 +266,24 @@ def test_mfma_bf16_dma_bit_identical_to_register_staging(case, pad, off):
                            ref.view(torch.int16 if od == torch.bfloat16 else torch.int32))
 
 
+@pytest.mark.parametrize("case", DMA_CASES)
+@pytest.mark.parametrize("env", [("HYGRID_CONV_WDB", "1"), ("HYGRID_CONV_NT", "2")])
+def test_mfma_bf16_dma_weight_buffering_and_tiles_bit_identical(case, env):
+    """The single-buffered weight chunks (default) and the double-buffered ones
+    (HYGRID_CONV_WDB=1) stage the same fragments for the same MFMAs: bit-identical outputs; two
+    output-channel tiles per workgroup (HYGRID_CONV_NT=2) compute each output's sum in the same
+    order: bit-identical too."""
+    B, C, O_, h, w = case
+    k, b = _weights(O_, C, h * 3 + w)
+    x = _bf16_input((B, C, h, w), h + 2 * w)
+    for od in (torch.float32, torch.bfloat16):
+        y = ops.hexconv2d(x, k, b, 0, 2, padding=1, out_dtype=od)
+        torch.cuda.synchronize()
+        ref = _with_env(env[0], env[1], ops.hexconv2d, x, k, b, 0, 2, padding=1, out_dtype=od)
+        assert torch.equal(y.view(torch.int16 if od == torch.bfloat16 else torch.int32),
+                           ref.view(torch.int16 if od == torch.bfloat16 else torch.int32))
+
+
 def test_mfma_bf16_dma_vs_oracle_and_unaligned():
     """1e-5 against the fp64 oracle on a shape with many interior tiles; a source that is
     2-B aligned only (odd element offset) keeps the register staging, same results."""
