@@ -59,6 +59,12 @@ namespace hg {
 #ifndef TU_ORDER
 #define TU_ORDER 0          // unit index -> (window fastest, band, chunk); 1: band fastest
 #endif
+#ifndef TU_VLD
+#define TU_VLD 1            // 1: input rows by dword loads into VGPRs, PDP planes ahead, written to a
+#endif                      // one-plane LDS slot when consumed (instead of LDS-DMA into a ring)
+#ifndef TU_PDP_VLD
+#define TU_PDP_VLD 4        // with TU_VLD: planes of rows held in VGPRs ahead of the one blended
+#endif
 #ifndef TU_DIAG
 #define TU_DIAG 0           // diagnostics (A/B variants only): 1 = no stores, 2 = no row loads, 3 = neither
 #endif
@@ -73,8 +79,8 @@ constexpr int TU_ROWB = TU_PCB + 16;         // ring bytes of one input row (+ a
 // < 64 outstanding), ring slots and bytes of one plane slot
 template <bool NEAR> struct TuCfg {
     static constexpr int RB = NEAR ? TU_RB_NEAR : TU_RB, NR = RB / 2 + 2;
-    static constexpr int PDP_ = NEAR ? 63 / (2 * NR + RB) : TU_PDP;
-    static constexpr int PDP = PDP_ < 6 ? PDP_ : 6, NP = PDP + 1, SLOT = NR * TU_ROWB;
+    static constexpr int PDP_ = TU_VLD ? TU_PDP_VLD : NEAR ? 63 / (2 * NR + RB) : TU_PDP;
+    static constexpr int PDP = PDP_ < 6 ? PDP_ : 6, NP = TU_VLD ? 1 : PDP + 1, SLOT = NR * TU_ROWB;
     static_assert(PDP >= 1 && PDP * (2 * NR + RB) < 64, "vmcnt");
 };
 
@@ -232,6 +238,75 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
             constexpr int N = decltype(Nc)::value;
             __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf) | ((N >> 4) << 14));
         };
+        // TU_VLD: the rows of PDP planes in VGPRs, slot pi % PDP; plane pi is written to the one
+        // LDS slot when its turn comes (the wave's LDS ops run in order: its gathers of plane
+        // pi - 1 are done, its gathers of plane pi see the writes)
+        unsigned rv[TU_VLD ? TU_PDP_ : 1][TU_VLD ? TU_NR_ : 1][2];
+        const unsigned voff1v = lane < 8 ? voff1 : 0x80000000u;
+        auto vld = [&](int pi, auto SLc) {
+            constexpr int SL = decltype(SLc)::value;
+            const unsigned po = pi < np ? (unsigned)pi * planeb : (unsigned)np * planeb;
+#pragma unroll
+            for (int q = 0; q < TU_NR_; ++q) {
+                const unsigned so = po + (unsigned)min(rlo + q, D.h - 1) * rowb;
+                rv[SL][q][0] = __builtin_amdgcn_raw_buffer_load_b32(xr, voff0, so, 0);
+                rv[SL][q][1] = __builtin_amdgcn_raw_buffer_load_b32(xr, voff1v, so, 0);
+            }
+        };
+        auto body_v = [&](int pi, auto SLc) {
+            constexpr int SL = decltype(SLc)::value;
+            // plane pi's loads are done once at most those issued after them are outstanding:
+            // the loads of the next PDP - 1 planes and the stores of the planes since
+            constexpr int NL = 2 * TU_NR_, NST = TU_RB_;
+            static_assert((TU_PDP_ - 1) * NL + TU_PDP_ * NST < 64, "vmcnt");
+            if (pi >= TU_PDP_) {
+                wait(std::integral_constant<int, (TU_PDP_ - 1) * NL + TU_PDP_ * NST>{});
+            } else {
+                tu_static_for<TU_PDP_>([&](auto Pc) {
+                    constexpr int P_ = decltype(Pc)::value;
+                    if (pi == P_) wait(std::integral_constant<int, (TU_PDP_ - 1) * NL + P_ * NST>{});
+                });
+            }
+#pragma unroll
+            for (int q = 0; q < TU_NR_; ++q) {
+                *reinterpret_cast<unsigned*>(ring + q * TU_ROWB + 4 * lane) = rv[SL][q][0];
+                if (lane < 8) *reinterpret_cast<unsigned*>(ring + q * TU_ROWB + 256 + 4 * lane) = rv[SL][q][1];
+            }
+            vld(pi + TU_PDP_, SLc);                         // the slot's registers are free again
+            const unsigned char* const sb = ring;
+            const unsigned so = (unsigned)pi * oplane;
+#pragma unroll
+            for (int k = 0; k < TU_RB_; ++k) {
+                unsigned pk[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int kk = 0; kk < K; ++kk) {
+                    unsigned bits;
+                    if constexpr (NEAR) {
+                        bits = *reinterpret_cast<const UIn*>(sb + off[k][kk][0]);
+                    } else {
+                        const float v0 = tu_f32<Tin>(*reinterpret_cast<const UIn*>(sb + off[k][kk][0]));
+                        const float v1 = tu_f32<Tin>(*reinterpret_cast<const UIn*>(sb + off[k][kk][1]));
+                        const float v2 = tu_f32<Tin>(*reinterpret_cast<const UIn*>(sb + off[k][kk][2]));
+                        bits = tu_bits<Tout>(wt[k][kk][0] * v0 + wt[k][kk][1] * v1 + wt[k][kk][2] * v2);   // :354
+                    }
+                    constexpr int SB = (int)sizeof(Tout) * 8;
+                    if constexpr (SB == 32) pk[kk] = bits;
+                    else pk[(kk * SB) / 32] |= bits << ((kk * SB) % 32);
+                }
+                tu_store<OB>(pk, yr, vo, __builtin_amdgcn_readfirstlane(so + yo[k]));
+            }
+        };
+        if constexpr (TU_VLD) {
+            tu_static_for<TU_PDP_>([&](auto Pc) { vld(decltype(Pc)::value, Pc); });   // prologue
+            int pi = 0;
+            for (; pi + TU_PDP_ <= np; pi += TU_PDP_)
+                tu_static_for<TU_PDP_>([&](auto Sc) { body_v(pi + decltype(Sc)::value, Sc); });
+            tu_static_for<TU_PDP_ - 1>([&](auto Sc) {
+                if (pi + decltype(Sc)::value < np) body_v(pi + decltype(Sc)::value, Sc);
+            });
+            __builtin_amdgcn_s_waitcnt(0x0f70);             // vmcnt(0): no load in flight at exit
+            continue;
+        }
         auto body = [&](int pi, auto SLc) {
             constexpr int SL = decltype(SLc)::value;
             dma(pi + TU_PDP_, std::integral_constant<int, (SL + TU_PDP_) % TU_NP_>{});
