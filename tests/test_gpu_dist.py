@@ -5,9 +5,12 @@ sharding logic at world 2 and 4 on the CPU; this runs the same calls through RCC
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
+
+from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -74,8 +77,9 @@ def test_rccl_world1_config3_shard(nccl_world1):
     """Config 4's per-rank workload through RCCL: one rank's 128 x 3 x 2160 x 3840 bf16 shard
     (config 3's batch) through the fused pipeline, then the bench's timed-loop collective
     (per-image sums of every 64th output row, all-gathered into a preallocated buffer) and
-    the checksum gather.  The sums must equal the local ones exactly, and three images of
-    the shard (first, middle, last) are checked against the operator chain."""
+    the checksum gather.  The sums must equal the local ones exactly, three images of the
+    shard (first, middle, last) are checked against the operator chain and the last one
+    against the fp64 oracle chain (one bf16 rounding)."""
     dev = nccl_world1
     torch.manual_seed(3)
     conv = HexConv2d(3, 3, 0, 2, padding=1, bias=True).to(dev)
@@ -99,4 +103,11 @@ def test_rccl_world1_config3_shard(nccl_world1):
             u = ops.hex_to_rect(conv(ops.rect_to_hex(xi, (2160, 3840), out_dtype=torch.float32)),
                                 (2160, 3840), out_dtype=torch.float32)
             torch.testing.assert_close(y[i:i + 1].float(), u, rtol=2 ** -7, atol=2 ** -7 * u.abs().max().item())
+    # and the shard's last image against the fp64 oracle chain: one bf16 rounding
+    h = O.rect_to_hex(mine[127].double().cpu().numpy(), (2160, 3840), 1)
+    c = O.hexconv2d(h, conv.kernel.detach().cpu().double().numpy(),
+                    conv.bias.detach().cpu().double().numpy(), 0, 2, padding=1)
+    ref = O.hex_to_rect(c, (2160, 3840), 1).reshape(3, 2160, 3840)
+    got = y[127].double().cpu().numpy()
+    assert np.abs(got - ref).max() <= 2.0 ** -8 * np.abs(ref).max()
     del x, y
