@@ -4,6 +4,9 @@
 // (4K bf16, 3 planes, B = 128, 128-column windows owning 120, 4 windows per workgroup,
 // XCD-swizzled group-fastest order, RB-row bands + 4 halo rows), no arithmetic.
 //   NB = 1 with PD = 3 is walk4/walk6's register-ring pattern (the fused kernel's today).
+//   ALT = 1: odd bands walk upwards (last row first), so a band and its upper neighbour read
+//   their 2 shared halo rows together at the end / start of both walks (L2 hits?); ALT = 2:
+//   every band walks upwards (control: same pattern, mirrored).
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
@@ -21,7 +24,7 @@ __device__ __forceinline__ unsigned xcd_swz(unsigned bid, unsigned nwg) {
 
 // rows s0 - 2 .. s1 + 1 are read (the band + 4 halo rows), rows s0 .. s1 - 1 stored; blocks of NB
 // rows: block k's loads are issued while block k - 1 is "processed" (stored)
-template <int RB, int NB>
+template <int RB, int NB, int ALT = 0>
 __global__ __launch_bounds__(256) void walk(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int B) {
     constexpr int NBND = (H + RB - 1) / RB;
     const int lane = threadIdx.x & 63;
@@ -46,10 +49,12 @@ __global__ __launch_bounds__(256) void walk(const uint16_t* __restrict__ x, uint
     unsigned acc = 0;
     unsigned cur[NB][C], nxt[NB][C];
     const int r0 = s0 - 2, r1 = s1 + 2;                  // rows read: r0 .. r1 - 1
+    const bool up = ALT == 2 || (ALT == 1 && (band & 1));
+    auto mrow = [&](int r) { return up ? r0 + r1 - 1 - r : r; };
     auto load_block = [&](int rb, unsigned (&d)[NB][C]) {
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
-            const unsigned so = roff(rb + i);
+            const unsigned so = roff(mrow(rb + i));
 #pragma unroll
             for (int c = 0; c < C; ++c) d[i][c] = __builtin_amdgcn_raw_buffer_load_b32(xr, xoff, so + c * xplane, 0);
         }
@@ -59,7 +64,7 @@ __global__ __launch_bounds__(256) void walk(const uint16_t* __restrict__ x, uint
         if (rb + NB < r1) load_block(rb + NB, nxt);
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
-            const int r = rb + i;
+            const int r = mrow(rb + i);
             const unsigned sw = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(r, 0), H - 1) * xrow));
             const bool st = r >= s0 && r < s1;
 #pragma unroll
@@ -91,11 +96,12 @@ float timeit(K k, int reps) {
 }
 
 static const double GB = 2.0 * 128 * C * H * W * 2 / 1e9;
-template <int RB, int NB>
+template <int RB, int NB, int ALT = 0>
 void run(const uint16_t* x, uint16_t* y, int B) {
     const int blocks = NGRP * ((H + RB - 1) / RB) * B;
-    const float ms = timeit([&] { hipLaunchKernelGGL((walk<RB, NB>), dim3(blocks), dim3(256), 0, 0, x, y, B); }, 9);
-    printf("RB %3d  rows per load/store batch %2d : %.3f ms  %.3f of 8 TB/s\n", RB, NB, ms, GB / ms * 1e3 / 8000);
+    const float ms = timeit([&] { hipLaunchKernelGGL((walk<RB, NB, ALT>), dim3(blocks), dim3(256), 0, 0, x, y, B); }, 9);
+    printf("RB %3d  rows per load/store batch %2d  %-12s: %.3f ms  %.3f of 8 TB/s\n", RB, NB,
+           ALT == 0 ? "all down" : ALT == 1 ? "alternating" : "all up", ms, GB / ms * 1e3 / 8000);
     fflush(stdout);
 }
 
@@ -116,12 +122,14 @@ int main() {
     printf("%-44s %.3f ms  %.3f of 8 TB/s\n", "one-shot float4 copy (ceiling)", mc, GB / mc * 1e3 / 8000);
     for (int rep = 0; rep < 2; ++rep) {
         run<42, 1>(x, y, B);
-        run<42, 2>(x, y, B);
-        run<42, 3>(x, y, B);
-        run<42, 6>(x, y, B);
-        run<42, 12>(x, y, B);
-        run<18, 6>(x, y, B);
-        run<96, 12>(x, y, B);
+        run<42, 1, 1>(x, y, B);
+        run<42, 1, 2>(x, y, B);
+        run<30, 1>(x, y, B);
+        run<30, 1, 1>(x, y, B);
+        run<18, 1>(x, y, B);
+        run<18, 1, 1>(x, y, B);
+        run<96, 1>(x, y, B);
+        run<96, 1, 1>(x, y, B);
     }
     return 0;
 }
