@@ -37,6 +37,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# What bounds the headline kernel, from the shipped build's code object (124 VGPRs, 102 SGPRs,
+# no spills: 4 waves per SIMD) and its SQ counters (profiles/r05/).
+FUSED4_LIMITER = ("VALU issue and memory together for the fused kernel (k_fused4: 4 columns per "
+                  "lane, 124 VGPRs, 4 waves per SIMD; 126 packed stencil FMAs + r2h / h2r per "
+                  "240-column wave-step, ~88 % of SIMD cycles issuing VALU)")
 PEAK_BPS = HBM_PEAK_GBS * 1e9
 
 
@@ -409,10 +414,7 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": traffic_note,
                 "alg_bytes_per_launch": alg_bytes[dom],
-                "limiter": "VALU issue and memory together for the fused kernel (k_fused4: 4 "
-                           "columns per lane, 150 VGPRs, 3 waves per SIMD; 126 packed stencil "
-                           "FMAs + r2h / h2r per 240-column wave-step); the 2-column kernel's "
-                           "cache-resident build ran 12-15 % faster than it (DESIGN.md section 6)"
+                "limiter": FUSED4_LIMITER
                 if dom == "pipeline_r2h_conv_h2r" else "hbm"}
 
     compare = None

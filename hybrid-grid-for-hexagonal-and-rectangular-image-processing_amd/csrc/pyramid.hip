@@ -76,6 +76,8 @@ struct PyrGeom {
     Geom r2h;                  // rect_to_hex lattice (h, w) -> (h, w) (from_rect)
     int cap_yr, cap_yc;        // Y footprint capacity (PY_YR, PY_YC; smaller only in tests)
     int* fault;                // set to 1 by a workgroup whose footprint overflows its tile
+                               // (null unless forced_cap: the host bound is exact)
+    int forced_cap;            // HYGRID_PYR_LDS_FORCE_CAP (tests): a tile below the bound
 };
 
 // r=2, padding-1 tap geometry (fused_kernel.h): tap t of an output row of parity `par`
@@ -208,7 +210,7 @@ __global__ __launch_bounds__(PY_THREADS) void k_pyr_level(const Tin* __restrict_
     // smaller cap), the workgroup raises the call's fault flag -- hg_hex_pyramid_level then
     // returns HG_EOVERFLOW -- and writes its outputs as NaN instead of leaving them unset.
     auto poison = [&]() {
-        if (tid == 0) atomicOr(G.fault, 1);
+        if (tid == 0 && G.fault) atomicOr(G.fault, 1);
         for (int64_t p = p0; p < p1; ++p)
             for (int k = tid; k < PY_TZR * PY_TZC; k += PY_THREADS) {
                 const int a = a0 + k / PY_TZC, b = b0 + k % PY_TZC;
@@ -437,30 +439,38 @@ static bool r2h_near_identity(const Geom& g) {
 // tile's footprint is the union over its rows: an exact bound on the kernel's reduction
 // (which counts only the vertices inside the raster), O(h1) per tile column.
 static bool pyr_footprint_ok(const Geom& g, int cap_r, int cap_c) {
+    // i_n(a) and j_n(a, b) exactly as tri_sample_xy computes them (the same fp64 expressions in
+    // the same order), without the rest of the sample: the row terms once per row, the y_ of
+    // every tile column's two end columns once per call, then two adds and a trunc per
+    // (row, tile column).
+    const double ch = (double)(g.h - 1) * 0.5, cw = (g.ww - 0.5) * 0.5;
     const int64_t nty = (g.h1 + PY_TZR - 1) / PY_TZR, ntx = (g.w1 + PY_TZC - 1) / PY_TZC;
-    for (int64_t ty = 0; ty < nty; ++ty) {
-        const int64_t a0 = ty * PY_TZR, a1 = std::min<int64_t>(a0 + PY_TZR, g.h1) - 1;
-        const TriSample s0 = tri_sample(g, a0, 0), s1 = tri_sample(g, a1, 0);
-        if (s1.i_n + 1 - s0.i_n + 1 > cap_r) return false;
-    }
-    std::vector<int64_t> lo(g.h1), hi(g.h1);
+    std::vector<double> y0(ntx), y1(ntx);
+    std::vector<int64_t> lo(ntx), hi(ntx);
     for (int64_t tx = 0; tx < ntx; ++tx) {
-        const int64_t b0 = tx * PY_TZC, b1 = std::min<int64_t>(b0 + PY_TZC, g.w1) - 1;
-        for (int64_t a = 0; a < g.h1; ++a) {
-            const TriSample s0 = tri_sample(g, a, b0), s1 = tri_sample(g, a, b1);
-            const int64_t q1 = (int64_t)((double)(s0.i_n + 1) / 2.0), q2 = (int64_t)((double)(s0.i_n + 2) / 2.0);
-            lo[a] = s0.j_n - q2;
-            hi[a] = s1.j_n + 1 - q1;
-        }
-        for (int64_t ty = 0; ty < nty; ++ty) {
-            const int64_t a0 = ty * PY_TZR, a1 = std::min<int64_t>(a0 + PY_TZR, g.h1);
-            int64_t l = INT64_MAX, u = INT64_MIN;
-            for (int64_t a = a0; a < a1; ++a) {
-                l = std::min(l, lo[a]);
-                u = std::max(u, hi[a]);
+        y0[tx] = axis_at(g.ys, tx * PY_TZC);
+        y1[tx] = axis_at(g.ys, std::min<int64_t>(tx * PY_TZC + PY_TZC, g.w1) - 1);
+    }
+    for (int64_t ty = 0; ty < nty; ++ty) {
+        const int64_t a0 = ty * PY_TZR, a1 = std::min<int64_t>(a0 + PY_TZR, g.h1);
+        std::fill(lo.begin(), lo.end(), INT64_MAX);
+        std::fill(hi.begin(), hi.end(), INT64_MIN);
+        int64_t in0 = 0, in1 = 0;
+        for (int64_t a = a0; a < a1; ++a) {
+            const double i_ = axis_at(g.xs, a) + ch;                              // :276
+            const int64_t in = (int64_t)i_;                                       // :280
+            if (a == a0) in0 = in;
+            in1 = in;
+            const int64_t q1 = (int64_t)((double)(in + 1) / 2.0), q2 = (int64_t)((double)(in + 2) / 2.0);
+            const double hi_ = 0.5 * i_;
+            for (int64_t tx = 0; tx < ntx; ++tx) {
+                lo[tx] = std::min(lo[tx], (int64_t)(hi_ + y0[tx] + cw) - q2);     // :277, :281
+                hi[tx] = std::max(hi[tx], (int64_t)(hi_ + y1[tx] + cw) + 1 - q1);
             }
-            if (u - l + 1 > cap_c) return false;
         }
+        if (in1 + 1 - in0 + 1 > cap_r) return false;       // i_n grows with the row
+        for (int64_t tx = 0; tx < ntx; ++tx)
+            if (hi[tx] - lo[tx] + 1 > cap_c) return false;
     }
     return true;
 }
@@ -472,7 +482,17 @@ static int pyr_launch(const void* src, void* dst, PyrGeom& G, hipStream_t st) {
     nchunk = std::min<int64_t>(nchunk, 65535);
     G.pc = (int)((G.planes + nchunk - 1) / nchunk);
     const dim3 grid((unsigned)tiles, (unsigned)((G.planes + G.pc - 1) / G.pc));
-    // the fault flag: one word per call (reentrant), read back after the launch
+    // The host bound (pyr_footprint_ok) is exact, so a launch it admitted never overflows its
+    // tile: production launches carry no fault word and never synchronise (a workgroup that
+    // overflowed anyway would still write NaN, never stale data).  Only under the test-only
+    // HYGRID_PYR_LDS_FORCE_CAP (a tile smaller than the bound) does the call allocate a fault
+    // word, read it back and return HG_EOVERFLOW.
+    if (!G.forced_cap) {
+        G.fault = nullptr;
+        hipLaunchKernelGGL((k_pyr_level<FR, OP, Tin, Tout>), grid, dim3(PY_THREADS), 0, st,
+                           (const Tin*)src, (Tout*)dst, G);
+        return launch_status();
+    }
     int* fault = nullptr;
     hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&fault), sizeof(int), st);
     if (e != hipSuccess) return (int)e;
@@ -559,6 +579,7 @@ static int pyr_level(const void* src, void* dst, int src_dtype, int dst_dtype, i
     const char* cap = getenv("HYGRID_PYR_LDS_FORCE_CAP");   // tests only
     if (cap && atoi(cap) > 0) {
         G.cap_yr = std::min(PY_YR, atoi(cap));
+        G.forced_cap = 1;
     } else if (!pyr_footprint_ok(G.tri, PY_YR, PY_YC)) {
         return HG_EUNSUP;
     }

@@ -113,7 +113,11 @@ int hg_resample_backward(int op, const void* gy, void* dx, int acc_dtype, int64_
  * resample_stream.hip), HG_KERNEL_DOWN (~2x downsampling streaming kernels: rect->hex,
  * resample_down.hip; hexresize (pyramid levels), hexresize_down.hip), HG_KERNEL_UP
  * (upsampling triangle lattices, linear and nearest: hex (h/2, w/2) -> rect (h, w), tri_up.hip), or a
- * negative status.  Introspection for tests and tools; the reference has no counterpart. */
+ * negative status.  Introspection for tests and tools; the reference has no counterpart.
+ * The query has no source pointer, so it answers for a source whose base is 16-B aligned (what
+ * torch allocations are); a real call with a 4-B but not 16-B aligned source (a sliced view)
+ * takes the hexresize streaming kernel's 4-B-piece layout, whose narrower windows can decline
+ * where the query said HG_KERNEL_DOWN: that call then runs the general kernel. */
 enum hg_kernel { HG_KERNEL_GENERAL = 0, HG_KERNEL_NEAREST = 1, HG_KERNEL_STREAM = 2,
                  HG_KERNEL_DOWN = 3, HG_KERNEL_UP = 4 };
 int hg_resample_kernel(int op, int src_dtype, int dst_dtype, int64_t planes, int64_t h, int64_t w,

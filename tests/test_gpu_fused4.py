@@ -69,9 +69,17 @@ def test_fused4_bit_identical_to_two_column_and_vs_oracle(shape, off, monkeypatc
     y4 = _run(x, conv, off, monkeypatch, False)
     y2 = _run(x, conv, off, monkeypatch, True)
     _same(y4, y2)
+    # What pins this kernel at the north_star's 1e-5 is the bit-identity above: the two-column
+    # kernel is oracle-checked at 1e-5 in fp32 (tests/test_gpu_pipeline.py).  Against the fp64
+    # oracle directly, each bf16 output is one rounding of an fp32 value within ~1e-6 of the
+    # oracle's: per element |got - ref| <= 2^-8 |ref| (half an ulp is 2^-9 |ref| at most; the
+    # fp32 error may tip a near-tie to the other neighbour) plus an absolute floor for values
+    # near zero, where the fp32 cancellation error is relative to the terms, not the sum.
     ref = _oracle(x[B - 1:B], conv)[0]
     got = y4[B - 1].double().cpu().numpy()
-    assert np.abs(got - ref).max() <= 2.0 ** -8 * np.abs(ref).max()
+    tol = 2.0 ** -8 * np.abs(ref) + 1e-5 * np.abs(ref).max()
+    bad = np.abs(got - ref) > tol
+    assert not bad.any(), f"{int(bad.sum())} outputs beyond one bf16 rounding of the oracle"
 
 
 @pytest.mark.parametrize("off", [0, 1])

@@ -2,7 +2,7 @@
 """Per-step instruction mix of a streaming kernel's row loop, from device assembly.
 
     hipcc --offload-arch=gfx950 ... --cuda-device-only -S fused.hip -o f.s
-    python tools/loop_mix.py f.s <kernel-name-substring> [steps_per_trip] [min_pk]
+    python tools/loop_mix.py f.s <kernel-name-substring> [steps_per_trip] [min_pk] [nloops]
 
 Finds every loop (a label with a later branch back to it) in the first kernel whose
 name contains the substring, keeps the innermost ones (no loop nested inside) and
@@ -46,7 +46,13 @@ def main():
     inner = [(a, b) for a, b in loops if not any(a < c and d < b for c, d in loops if (c, d) != (a, b))]
     if not inner:
         raise SystemExit("no loop")
-    a, b = max(inner, key=lambda ab: ab[1] - ab[0])
+    inner.sort(key=lambda ab: ab[1] - ab[0], reverse=True)
+    nloops = int(sys.argv[5]) if len(sys.argv) > 5 else 1      # report the N largest loops
+    for a, b in inner[:nloops]:
+        report(name, body, a, b, steps)
+
+
+def report(name, body, a, b, steps):
     cnt = Counter()
     for ln in body[a:b + 1]:
         t = ln.strip()
