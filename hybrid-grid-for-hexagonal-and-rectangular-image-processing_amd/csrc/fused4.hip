@@ -40,6 +40,16 @@ namespace hg {
 #ifndef F4_WPE
 #define F4_WPE 4                       // waves per SIMD asked of the register allocator
 #endif
+#ifndef F4_DMA
+#define F4_DMA 0                       // rect rows by per-wave LDS-DMA into a 6-row LDS ring (2-3
+                                       // steps ahead, no VGPRs, no workgroup barrier) instead of
+                                       // the register ring
+#endif
+#ifndef F4_NOMEM
+#define F4_NOMEM 0                     // diagnostic floor: every row load / store hits row 0 of its
+                                       // plane (cache-resident), the arithmetic unchanged (1: loads
+                                       // and stores, 2: loads only, 3: stores only)
+#endif
 constexpr int F4_GW = 4, F4_THREADS = 256;
 constexpr int F4_HL = 8, F4_OWN = 240;  // window halo (left) and owned columns
 constexpr int F4_RB = F4_RB_;
@@ -61,9 +71,17 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     static_assert(PD >= 1 && PD <= 4, "raw ring: rows a2+2 .. a2+1+PD in flight in 6 slots");
     constexpr int NLUT_MAX = F4_RB + 2;
     __shared__ float4 lut_all[F4_GW][NLUT_MAX];
+    // DMA: per wave 6 row slots of 3 x 512 B (plane c of rect row R at slot (R - s0 + 2) % 6,
+    // bytes c * 512 + 8 * lane = this lane's 4 columns); pairs of slots (0,1) (2,3) (4,5) are
+    // contiguous, so two rows are three 1-KiB LDS-DMA pieces
+    constexpr bool DMA = F4_DMA;
+    constexpr int RSLOT = 3 * 512;
+    __shared__ __attribute__((aligned(16))) unsigned char ring_all[DMA ? F4_GW : 1][DMA ? 6 * RSLOT : 16];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4* const lut = lut_all[wslot];
+    const unsigned char* const ring = ring_all[DMA ? wslot : 0];
+    const unsigned ring_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)ring_all[DMA ? wslot : 0];
     const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
     const int ngrp = (F.nwin + F4_GW - 1) / F4_GW;
     // block -> (window group, band, image): group fastest (F4_ORDER 0) or band fastest (1: the
@@ -155,7 +173,48 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     const unsigned xplane = (unsigned)(cstride * 2), yplane = (unsigned)(ostride * 2);
     const unsigned xrow = (unsigned)F.w * 2u, yrow = (unsigned)F.w2 * 2u;
     auto row_off = [&](int k) -> unsigned {
+        if (F4_NOMEM == 1 || F4_NOMEM == 2) return 0u;
         return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(k, 0), F.h - 1) * xrow));
+    };
+    // DMA: piece j of a row pair (A, B) is 1 KiB: half-wave h (lanes 32 h .. 32 h + 31) moves the
+    // 512-B plane row 2 j + h of [A0 A1 A2 B0 B1 B2], lane l the 16 B of columns W0 + 8 (l % 32)
+    // .. + 7; columns left or right of the raster are out of the buffer range (zeros)
+    const int dgc = W0 + 8 * (lane & 31);
+    const unsigned dcol = (dgc >= 0 && dgc < F.w) ? (unsigned)dgc * 2u : 0x80000000u;
+    const bool dhi = lane >= 32;
+    const unsigned dv0 = dcol + (dhi ? xplane : 0u);              // A0 | A1   (+ row A)
+    const unsigned dv1 = dcol + (dhi ? 0u : 2u * xplane);         // A2 | B0   (+ row A, hi: + B - A)
+    const unsigned dv2 = dcol + (dhi ? 2u * xplane : xplane);     // B1 | B2   (+ row B)
+    // rows R, R + 1 into the slot pair starting at even slot PS (inline asm: hipcc does not see
+    // these loads, so it adds no vmcnt(0) before LDS reads; the waits are counted in step())
+    auto dma_pair = [&](int R, auto PSc) {
+        constexpr int PS = decltype(PSc)::value;
+        const unsigned rA = row_off(R), rB = row_off(R + 1);
+        const unsigned v1 = dv1 + (dhi ? rB - rA : 0u);
+        const unsigned l0 = (unsigned)__builtin_amdgcn_readfirstlane((int)(ring_lds + PS * RSLOT));
+        const unsigned l1 = l0 + 1024u, l2 = l0 + 2048u;
+        unsigned keep;
+        const unsigned a0 = dv0, a2 = dv2;
+        const __amdgpu_buffer_rsrc_t rs = xrs;
+        asm volatile("s_mov_b32 %0, m0\n\t"
+                     "s_mov_b32 m0, %4\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %1, %7, %8 offen lds\n\t"
+                     "s_mov_b32 m0, %5\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %2, %7, %8 offen lds\n\t"
+                     "s_mov_b32 m0, %6\n\t"
+                     "s_nop 0\n\t"
+                     "buffer_load_dwordx4 %3, %7, %9 offen lds\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(a0), "v"(v1), "v"(a2), "s"(l0), "s"(l1), "s"(l2), "s"(rs), "s"(rA), "s"(rB)
+                     : "memory");
+    };
+    auto dma_read = [&](int R, f4_u2 (&r)[3]) {
+        const unsigned char* const src = ring + fu_mod(R - s0 + 2, 6) * RSLOT + 8 * lane;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) r[c] = *reinterpret_cast<const f4_u2*>(src + c * 512);
     };
 
     // ---- weights (21 pairs in SGPRs, the rest opaque VGPR pairs) and bias ---------------
@@ -295,7 +354,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
         auto out_row = [&](auto PHc, int a2) {
             constexpr int PH = decltype(PHc)::value;
             constexpr int S0 = PH % 3;
-            const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
+            const unsigned so = (F4_NOMEM == 1 || F4_NOMEM == 3) ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
 #pragma unroll
             for (int o = 0; o < O; ++o) {
                 const fu_f2 zA = ZA[S0][o], zB = ZB[S0][o];
@@ -319,6 +378,28 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
         };
 
         // ---- prologue: u rows s0-1 and s0 -----------------------------------------------
+        if constexpr (DMA) {
+            dma_pair(s0 - 2, IC<0>{});
+            dma_pair(s0, IC<2>{});
+            dma_pair(s0 + 2, IC<4>{});
+            __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
+            asm volatile("" ::: "memory");
+            f4_u2 t0[C], t1[C], t2[C];
+            dma_read(s0 - 2, t0);
+            dma_read(s0 - 1, t1);
+            dma_read(s0, t2);
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                f4_unpack(t0[c], XA[1][c], XB[1][c], hi16);   // row s0-2 -> slot 1
+                f4_unpack(t1[c], XA[2][c], XB[2][c], hi16);   // row s0-1 -> slot 2
+                f4_unpack(t2[c], XA[0][c], XB[0][c], hi16);   // row s0   -> slot 0
+            }
+            urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});
+            dma_read(s0 + 1, t0);
+#pragma unroll
+            for (int c = 0; c < C; ++c) f4_unpack(t0[c], XA[1][c], XB[1][c], hi16);   // row s0+1
+            urow(IC<-1>{}, lut[1], std::true_type{}, std::false_type{});
+        } else {
         {
             f4_u2 t0[C], t1[C], t2[C];
             const unsigned o0 = row_off(s0 - 2), o1 = row_off(s0 - 1), o2 = row_off(s0);
@@ -347,14 +428,31 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
         convert(IC<1>{}, IC<1>{});                                      // row s0+1 -> slot 1
         urow(IC<-1>{}, lut[1], std::true_type{}, std::false_type{});    // u row s0: above, centre
         __builtin_amdgcn_s_waitcnt(0x0f70);                             // vmcnt(0)
+        }
 
         // ---- main loop -----------------------------------------------------------------
         float4 lnext = lut[2];
         auto step = [&](auto PHc, int a2) {
             constexpr int PH = decltype(PHc)::value;
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (DMA) {
+                // rect row a2+2 landed once at most the operations issued after its last piece
+                // are outstanding (vmcnt counts LDS-DMA and stores together, in issue order):
+                // even steps read the first row of the pair issued two steps back (after its
+                // piece 1: piece 2 + 2 x 3 stores), odd steps the second row of the pair issued
+                // three steps back (after piece 2: 3 x 3 stores + one pair); the prologue drains
+                constexpr int N = (PH & 1) ? 12 : 7;
+                __builtin_amdgcn_s_waitcnt(0x0f70 & ~0xf | (N & 0xf));
+                asm volatile("" ::: "memory");
+                f4_u2 r[C];
+                dma_read(a2 + 2, r);
+#pragma unroll
+                for (int c = 0; c < C; ++c) f4_unpack(r[c], XA[(PH + 2) % 3][c], XB[(PH + 2) % 3][c], hi16);
+                if constexpr ((PH & 1) == 0) dma_pair(a2 + 4, IC<PH % 6>{});   // rows a2+4, a2+5
+            } else {
             convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row a2+2
             issue(IC<(PH + 2 + PD) % 6>{}, a2 + 2 + PD);
+            }
             const float4 L = lnext;
             lnext = lut[min(a2 - s0 + 3, NLUT - 1)];
             urow(PHc, L, std::true_type{}, std::true_type{});           // u row a2+1
@@ -385,6 +483,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
         int base = s0;
         for (; base + 6 <= s1; base += 6) block6(base);
         tail(base);
+        if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): no LDS-DMA in flight at exit
     };
     if (cd == 1 && rc == 1) run(IC<1>{}, IC<1>{});
     else if (cd == 1 && rc == 2) run(IC<1>{}, IC<2>{});

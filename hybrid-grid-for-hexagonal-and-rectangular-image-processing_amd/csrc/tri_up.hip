@@ -374,7 +374,8 @@ static int tu_launch(const void* src, void* dst, TriUpGeom& D, hipStream_t st) {
     D.pc = (int)((D.planes + nchunk - 1) / nchunk);
     nchunk = (D.planes + D.pc - 1) / D.pc;
     D.units = tiles * nchunk;
-    const int64_t waves = std::min<int64_t>(D.units, RESIDENT);
+    int64_t waves = std::min<int64_t>(D.units, RESIDENT);
+    if (env_is("HYGRID_TU_GRID", "1")) waves = std::min<int64_t>(D.units, (int64_t)1 << 30);   // A/B: a wave per unit
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     hipLaunchKernelGGL((k_tri_up<Tin, Tout, K, NEAR>), dim3(blocks), dim3(TU_THREADS), 0, st,
                        (const Tin*)src, (Tout*)dst, D);

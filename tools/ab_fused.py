@@ -56,9 +56,9 @@ def main():
         rng.shuffle(order)               # no fixed position in the round (clock / heat drift)
         rt = {}
         for n, f in order:
-            env = n.split("%")[1].split("=") if "%" in n else None
-            if env:
-                os.environ[env[0]] = env[1]
+            env = [kv.split("=") for kv in n.split("%")[1:]]   # name%VAR=VAL[%VAR2=VAL2...]
+            for k_, v_ in env:
+                os.environ[k_] = v_
             for rep in range(3):         # back-to-back launches; the last one is timed
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -66,8 +66,8 @@ def main():
                 e1.record()
                 if rc != 0:
                     raise SystemExit(f"{n}: status {rc}")
-            if env:
-                del os.environ[env[0]]
+            for k_, _ in env:
+                del os.environ[k_]
             e1.synchronize()
             rt[n] = e0.elapsed_time(e1)
             if r == rounds:
