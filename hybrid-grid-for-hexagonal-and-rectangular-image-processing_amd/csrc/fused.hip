@@ -189,10 +189,12 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
 namespace hg {
 void fused4_layout(int* band_rows, int* win_own, int* win_halo);
 void rt4_layout(int* band_rows, int* win_own, int* win_halo);
+void fconv4_layout(int* band_rows, int* win_own, int* win_halo);
 }
 
 // md 0-2: the two-column kernel's modes; md 6: MD 0's four-column variant (fused4.hip: bf16,
-// C = O = 3, widths a multiple of 4); md 7: MD 2's four-column variant (rt4.hip)
+// C = O = 3, widths a multiple of 4); md 7: MD 2's four-column variant (rt4.hip); md 8: MD 1's four-column
+// variant (fused4.hip: bf16, C = O = 3)
 extern "C" int hg_fused_layout(int md, int* band_rows, int* win_own, int* win_halo) {
     if (!band_rows || !win_own || !win_halo) return HG_EINVAL;
     if (md == 6) {
@@ -201,6 +203,10 @@ extern "C" int hg_fused_layout(int md, int* band_rows, int* win_own, int* win_ha
     }
     if (md == 7) {
         hg::rt4_layout(band_rows, win_own, win_halo);
+        return HG_OK;
+    }
+    if (md == 8) {
+        hg::fconv4_layout(band_rows, win_own, win_halo);
         return HG_OK;
     }
     if (md < 0 || md > 2) return HG_EINVAL;

@@ -53,6 +53,11 @@ namespace hg {
 constexpr int F4_GW = 4, F4_THREADS = 256;
 constexpr int F4_HL = 8, F4_OWN = 240;  // window halo (left) and owned columns
 constexpr int F4_RB = F4_RB_;
+#ifndef F4_RB_CONV_
+#define F4_RB_CONV_ 18                 // MD 1: output rows per band (k_fused MD 1's fastest)
+#endif
+constexpr int F4_RB_CONV = F4_RB_CONV_;
+static_assert(F4_RB_CONV % 6 == 0 && F4_RB_CONV > 0, "bands are whole 6-step blocks");
 static_assert(F4_RB % 6 == 0 && F4_RB > 0, "bands are whole 6-step blocks");
 
 typedef unsigned f4_u2 __attribute__((ext_vector_type(2)));
@@ -62,14 +67,19 @@ __device__ __forceinline__ void f4_unpack(f4_u2 r, fu_f2& a, fu_f2& b, unsigned 
     b = fu_f2{__builtin_bit_cast(float, r.y << 16), __builtin_bit_cast(float, r.y & hi16)};
 }
 
-template <int OP>
+// MD 0: rect -> hex -> HexConv2d -> hex -> rect (the headline).  MD 1: HexConv2d alone
+// (HexFrames.py:96-169, radius 2, stride 1, padding 1, pad value 0), as k_fused MD 1: the u rows
+// are the input rows (zeros outside the raster), no r2h / h2r, the conv rows stored as they
+// complete; the band length is F4_RB_CONV.
+template <int OP, int MD>
 __global__ __launch_bounds__(F4_THREADS) __attribute__((amdgpu_waves_per_eu(F4_WPE)))
 void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
               const float* __restrict__ bias, __bf16* __restrict__ y, FusedGeom F) {
     constexpr int C = 3, O = 3;
+    constexpr bool UIN = MD == 1;                    // u rows = input rows
     constexpr int PD = F4_PD;
     static_assert(PD >= 1 && PD <= 4, "raw ring: rows a2+2 .. a2+1+PD in flight in 6 slots");
-    constexpr int NLUT_MAX = F4_RB + 2;
+    constexpr int NLUT_MAX = (F4_RB > F4_RB_CONV ? F4_RB : F4_RB_CONV) + 2;
     __shared__ float4 lut_all[F4_GW][NLUT_MAX];
     // DMA: per wave 6 row slots of 3 x 512 B (plane c of rect row R at slot (R - s0 + 2) % 6,
     // bytes c * 512 + 8 * lane = this lane's 4 columns); pairs of slots (0,1) (2,3) (4,5) are
@@ -93,7 +103,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     const int win = grp * F4_GW + wslot;             // may be >= nwin: runs, owns nothing
     const int W0 = win * F4_OWN - F4_HL;
     const int ce = W0 + 4 * lane;                    // columns ce .. ce + 3 (pairs A, B)
-    constexpr int RB = F4_RB, NLUT = RB + 2;
+    constexpr int RB = MD == 1 ? F4_RB_CONV : F4_RB, NLUT = RB + 2;
     const int s0 = band * RB;
     const int s1 = min(s0 + RB, F.h2);
 
@@ -101,7 +111,9 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     for (int e = lane; e < NLUT; e += 64) {
         const int r = s0 - 1 + e;
         float4 t = {0.f, 0.f, 0.f, 0.f};
-        if (r >= 0 && r < F.h1) {
+        if (UIN) {
+            t.y = (r >= 0 && r < F.h) ? 1.f : 0.f;       // u row r = input row r; 0: padding row
+        } else if (r >= 0 && r < F.h1) {
             const double i_ = axis_at(F.rxs, r) + (double)(F.h - 1) * 0.5;   // :440
             const int in = (int)i_;                                          // :444
             const double f = i_ - (double)(float)in;                         // :448
@@ -115,7 +127,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     int rc = 0;
-    {
+    if (!UIN) {
         bool has_a = false, has_c = false;
         for (int e = lane; e < NLUT; e += 64) {
             const float4 t = lut[e];
@@ -137,7 +149,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             float* wr = s ? wo[k] : we[k];
             wr[0] = wr[1] = wr[2] = 0.f;
             const int q = ce + 2 * k + s;
-            if (q >= 0 && q < F.w1) {
+            if (!UIN && q >= 0 && q < F.w1) {
                 const double j_ = axis_at(F.rys, q) + (double)(F.w - 1) * 0.5;   // :441
                 const int jn = (int)j_;
                 const double jf = j_ - (double)(float)jn;
@@ -156,6 +168,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     const bool any_r = __builtin_amdgcn_ballot_w64(we[0][2] != 0.f || wo[0][2] != 0.f ||
                                                    we[1][2] != 0.f || wo[1][2] != 0.f) != 0;
     const int cd = !any_r ? 1 : (!any_l ? 2 : 0);
+    const bool colin = ce >= 0 && ce < F.w;          // MD 1: the lane's input columns (w % 4 == 0)
 
     // owned lanes 2 .. 61 (w2 % 4 == 0: a lane is wholly inside or outside the raster)
     const bool own = lane >= F4_HL / 4 && lane < (F4_HL + F4_OWN) / 4 && ce >= 0 && ce < F.w2 &&
@@ -233,7 +246,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     }
     float bv[O];
 #pragma unroll
-    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] * 0.75f : 0.f;
+    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] * (MD == 0 ? 0.75f : 1.f) : 0.f;
     fu_f2 bvp[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -279,6 +292,17 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             const fu_f2 Lxy = {L.x, L.y}, Lzw = {L.z, L.w};
             fu_sfor<0, C>([&](auto Cc) {
                 constexpr int c = decltype(Cc)::value;
+                float ue[2], uo[2];
+                if constexpr (UIN) {                // MD 1: u = input row r, 0 outside (padding 1)
+                    if constexpr (RC == 1) {        // interior band and window: no selects
+                        ue[0] = XA[S1][c].x; uo[0] = XA[S1][c].y;
+                        ue[1] = XB[S1][c].x; uo[1] = XB[S1][c].y;
+                    } else {
+                        const bool in_ = colin && L.y != 0.f;
+                        ue[0] = in_ ? XA[S1][c].x : 0.f; uo[0] = in_ ? XA[S1][c].y : 0.f;
+                        ue[1] = in_ ? XB[S1][c].x : 0.f; uo[1] = in_ ? XB[S1][c].y : 0.f;
+                    }
+                } else {
                 // vertical blend, packed (k_fused FU_VPK), for both pairs
                 auto vblend = [&](const fu_f2 (&X)[3][C]) {
                     if constexpr (RC == 1) return fu_pfma<1, false>(Lxy, X[S1][c], fu_pmul<0>(Lxy, X[S0][c]));
@@ -288,7 +312,6 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
                 const fu_f2 VA = vblend(XA), VB = vblend(XB);
                 // horizontal blend: columns ce .. ce+3 = VA.x VA.y VB.x VB.y; the lane's left
                 // neighbour column is the previous lane's VB.y, its right one the next lane's VA.x
-                float ue[2], uo[2];
                 if constexpr (CD == 1) {            // taps q-1, q
                     ue[0] = fmaf(we[0][1], VA.x, we[0][0] * f_prev(VB.y));
                     uo[0] = fmaf(wo[0][1], VA.y, wo[0][0] * VA.x);
@@ -305,6 +328,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
                     uo[0] = fmaf(wo[0][2], VB.x, fmaf(wo[0][1], VA.y, wo[0][0] * VA.x));
                     ue[1] = fmaf(we[1][2], VB.y, fmaf(we[1][1], VB.x, we[1][0] * VA.y));
                     uo[1] = fmaf(wo[1][2], nx, fmaf(wo[1][1], VB.y, wo[1][0] * VB.x));
+                }
                 }
                 // the stencil's column-shifted pairs (u[ce+s], u[ce+1+s]) for both pairs:
                 // s = 0: own; s = 1: (uo_k, ue_{k+1}); s = -1: (uo_{k-1}, ue_k); s = 2: pair k+1
@@ -359,7 +383,9 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             for (int o = 0; o < O; ++o) {
                 const fu_f2 zA = ZA[S0][o], zB = ZB[S0][o];
                 float o0, o1, o2, o3;
-                if constexpr ((PH & 1) == 0) {
+                if constexpr (MD == 1) {            // HexConv2d output row as is
+                    o0 = zA.x; o1 = zA.y; o2 = zB.x; o3 = zB.y;
+                } else if constexpr ((PH & 1) == 0) {
                     o0 = fmaf(c13, zA.y, zA.x);
                     o1 = fmaf(c13, zB.x, zA.y);
                     o2 = fmaf(c13, zB.y, zB.x);
@@ -442,7 +468,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
                 // piece 1: piece 2 + 2 x 3 stores), odd steps the second row of the pair issued
                 // three steps back (after piece 2: 3 x 3 stores + one pair); the prologue drains
                 constexpr int N = (PH & 1) ? 12 : 7;
-                __builtin_amdgcn_s_waitcnt(0x0f70 & ~0xf | (N & 0xf));
+                __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf));
                 asm volatile("" ::: "memory");
                 f4_u2 r[C];
                 dma_read(a2 + 2, r);
@@ -485,6 +511,15 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
         tail(base);
         if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): no LDS-DMA in flight at exit
     };
+    if constexpr (UIN) {
+        (void)cd; (void)rc;
+        // every u row of the band (s0 - 1 .. s1) and every lane's columns inside the input: the
+        // padding selects drop out (RC 1 marks that loop for MD 1)
+        const bool inner = s0 >= 1 && s1 + 1 <= F.h && __builtin_amdgcn_ballot_w64(!colin) == 0;
+        if (inner) run(IC<0>{}, IC<1>{});
+        else run(IC<0>{}, IC<0>{});
+        return;
+    }
     if (cd == 1 && rc == 1) run(IC<1>{}, IC<1>{});
     else if (cd == 1 && rc == 2) run(IC<1>{}, IC<2>{});
     else if (cd == 2 && rc == 1) run(IC<2>{}, IC<1>{});
@@ -506,9 +541,34 @@ int fused4_try(const void* x, const float* k, const float* bias, void* y, int x_
     if (blocks > INT_MAX) return HG_EUNSUP;
     const dim3 grid((unsigned)blocks), blk(F4_THREADS);
     if (op)
-        hipLaunchKernelGGL((k_fused4<1>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
+        hipLaunchKernelGGL((k_fused4<1, 0>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
     else
-        hipLaunchKernelGGL((k_fused4<0>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
+        hipLaunchKernelGGL((k_fused4<0, 0>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
+    return launch_status();
+}
+
+// HexConv2d alone (radius 2, stride 1, padding 1, pad value 0, no epilogue) on the 4-column
+// kernel (MD 1): bf16 in and out, C = O = 3, groups 1, w a multiple of 4; HG_EUNSUP otherwise
+// (the caller runs k_fused MD 1).  op = tap column class at padding 1 ((off + 1) & 1).
+int fconv4_try(const void* x, const float* k, const float* bias, void* y, int x_dtype, int y_dtype,
+               int64_t batch, int C, int O, int G, int64_t h, int64_t w, int op, hipStream_t st) {
+    if (env_is("HYGRID_FCONV4", "0")) return HG_EUNSUP;   // A/B switch: the 2-column kernel
+    if (x_dtype != HG_BF16 || y_dtype != HG_BF16 || C != 3 || O != 3 || G != 1) return HG_EUNSUP;
+    if ((w % 4) || w < 4 || h < 1 || batch < 1) return HG_EUNSUP;
+    if (3 * h * w * 2 >= ((int64_t)1 << 31)) return HG_EUNSUP;   // 32-bit offsets per image
+    FusedGeom F = {};
+    F.B = batch;
+    F.h = F.h1 = F.h2 = (int)h;
+    F.w = F.w1 = F.w2 = (int)w;
+    F.nwin = (int)((w + F4_OWN - 1) / F4_OWN);
+    F.nband = (int)((h + F4_RB_CONV - 1) / F4_RB_CONV);
+    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + F4_GW - 1) / F4_GW);
+    if (blocks > INT_MAX) return HG_EUNSUP;
+    const dim3 grid((unsigned)blocks), blk(F4_THREADS);
+    if (op)
+        hipLaunchKernelGGL((k_fused4<1, 1>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
+    else
+        hipLaunchKernelGGL((k_fused4<0, 1>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
     return launch_status();
 }
 
@@ -519,6 +579,12 @@ namespace hg {
 // place edge inputs from it)
 void fused4_layout(int* band_rows, int* win_own, int* win_halo) {
     *band_rows = F4_RB;
+    *win_own = F4_OWN;
+    *win_halo = F4_HL;
+}
+// the same for the HexConv2d mode (hg_fused_layout(8, ...))
+void fconv4_layout(int* band_rows, int* win_own, int* win_halo) {
+    *band_rows = F4_RB_CONV;
     *win_own = F4_OWN;
     *win_halo = F4_HL;
 }

@@ -313,6 +313,8 @@ static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st)
     const int64_t upw = ue ? std::max(1, atoi(ue)) : 1;
     const int64_t tiles = (int64_t)D.nwin * D.nband;
     int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, (upw * RESIDENT + tiles - 1) / tiles));
+    if (const char* e = getenv("HYGRID_TSK_CHUNKS"))   // A/B switch: plane chunks per tile
+        nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, atoi(e)));
     // a chunk's planes are one buffer each way: 32-bit offsets, including the planes past
     // the chunk the prefetch addresses (out of range: zeros)
     const int64_t plane_bytes = std::max<int64_t>((int64_t)D.h * D.w * 2, (int64_t)D.h1 * D.w1 * 4);
@@ -321,7 +323,8 @@ static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st)
     D.pc = (int)((D.planes + nchunk - 1) / nchunk);
     D.nchunk = (int)((D.planes + D.pc - 1) / D.pc);
     D.units = tiles * D.nchunk;
-    const int64_t waves = std::min<int64_t>(D.units, RESIDENT);
+    int64_t waves = std::min<int64_t>(D.units, RESIDENT);
+    if (env_is("HYGRID_TSK_GRID", "1")) waves = std::min<int64_t>(D.units, (int64_t)1 << 30);   // A/B: a wave per unit
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     hipLaunchKernelGGL((k_hexresize_down<Tin, Tout, K, DB, P, SEP>), dim3(blocks), dim3(HD_THREADS), 0, st,
                        (const Tin*)src, (Tout*)dst, D);

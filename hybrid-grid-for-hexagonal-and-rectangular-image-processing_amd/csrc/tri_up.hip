@@ -30,8 +30,9 @@
 // 0.61 ms, while the stores alone take 0.29 ms (0.70 of 8 TB/s) and the arithmetic alone
 // 0.31 ms; deeper prefetch (2 -> 6 planes), 16-B DMA pieces, other unit orders, 4- and 6-row
 // bands and narrower windows did not move the mixed pattern below 0.41-0.48 ms.
-// Chunks are sized so the units about fill the resident waves once (records amortised over
-// as many planes as possible); waves stride over units.
+// Chunks (round 5): ~TU_CPP planes per unit and one wave per unit when the call has enough
+// planes (records amortised over >= 24 planes, short-lived waves); otherwise the units about
+// fill the resident waves once and waves stride over units.
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -64,6 +65,9 @@ namespace hg {
 #endif                      // one-plane LDS slot when consumed (instead of LDS-DMA into a ring)
 #ifndef TU_PDP_VLD
 #define TU_PDP_VLD 4        // with TU_VLD: planes of rows held in VGPRs ahead of the one blended
+#endif
+#ifndef TU_CPP
+#define TU_CPP 24           // planes per unit when the grid has a wave per unit (round 5)
 #endif
 #ifndef TU_DIAG
 #define TU_DIAG 0           // diagnostics (A/B variants only): 1 = no stores, 2 = no row loads, 3 = neither
@@ -360,9 +364,20 @@ template <typename Tin, typename Tout, int K, bool NEAR>
 static int tu_launch(const void* src, void* dst, TriUpGeom& D, hipStream_t st) {
     // units ~ the resident waves (256 CUs x 4 SIMDs x 4): plane chunks only when the tiles
     // alone leave most of them idle (the records are recomputed per chunk)
+    // Round 5: a unit is (window, band, chunk of ~TU_CPP planes) and the grid has one wave per
+    // unit (no wave strides over units): the records are amortised over >= 24 planes and the
+    // short-lived waves stream better than resident waves walking all planes (4K b32 linear:
+    // 0.592 -> 0.546 ms; 8 planes per chunk: 0.773, records dominate; profiles/r05/triup_grid_ab.txt).
+    // Calls with few planes keep the old rule: chunks until the units about fill the resident
+    // waves once, waves striding over units.
     constexpr int64_t RESIDENT = 256 * 4 * 4;
     const int64_t tiles = (int64_t)D.nwin * D.nband;
     int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, (RESIDENT + tiles / 2) / tiles));
+    bool grid = false;
+    if (!env_is("HYGRID_TU_GRID", "0") && D.planes >= 2 * TU_CPP) {
+        nchunk = std::max<int64_t>(nchunk, D.planes / TU_CPP);
+        grid = true;
+    }
     if (const char* e = getenv("HYGRID_TU_CHUNKS"))   // A/B switch: plane chunks per tile
         nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, atoi(e)));
     // a chunk's planes are one buffer each way: 32-bit offsets, including the planes past the
@@ -375,7 +390,7 @@ static int tu_launch(const void* src, void* dst, TriUpGeom& D, hipStream_t st) {
     nchunk = (D.planes + D.pc - 1) / D.pc;
     D.units = tiles * nchunk;
     int64_t waves = std::min<int64_t>(D.units, RESIDENT);
-    if (env_is("HYGRID_TU_GRID", "1")) waves = std::min<int64_t>(D.units, (int64_t)1 << 30);   // A/B: a wave per unit
+    if (grid || env_is("HYGRID_TU_GRID", "1")) waves = std::min<int64_t>(D.units, (int64_t)1 << 30);
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     hipLaunchKernelGGL((k_tri_up<Tin, Tout, K, NEAR>), dim3(blocks), dim3(TU_THREADS), 0, st,
                        (const Tin*)src, (Tout*)dst, D);

@@ -7,7 +7,7 @@ usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
   OP: r2h | h2r | conv | wide (HexConv2d 64->64, 1080p bf16 b4) | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1 | pyr2   (bf16 4K b128 for
       r2h/h2r/conv; fp32 1080p b32 for r2h32/h2r32 and rt, the fused round trip; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K from a
       hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K, pyr2 = level 2, 2K -> 1K;
-      hr0 / hr1 / hr2 = hexresize alone at those three levels (fp16); up = hex (h/2, w/2) -> rect (h, w)
+      hr0 / hr1 / hr2 = hexresize alone at those three levels (fp16); hrb = 4K -> 2K bf16 b32; up = hex (h/2, w/2) -> rect (h, w)
       linear at 4K bf16 b32, the inverse of ConvertToHexagon's lattice)
   name 'base' = the in-tree library; others = HyGrid/_lib/variants/libhygrid_<name>.so;
   'name%VAR=VAL' runs that library with the environment variable VAR=VAL set around its calls
@@ -57,6 +57,8 @@ def main():
         B, C, H, W, t = 32, 3, 1080, 1920, torch.bfloat16
     elif op == "upn":
         B, C, H, W, t = 32, 3, 1080, 1920, torch.uint8
+    elif op == "hrb":                  # the bench's hexresize_2x line: 4K -> 2K bf16 b32
+        B, C, H, W, t = 32, 3, 2160, 3840, torch.bfloat16
     else:
         B, C, H, W, t = 8, 3, 4320, 7680, torch.float16
     if t == torch.uint8:
