@@ -552,7 +552,9 @@ int fused4_try(const void* x, const float* k, const float* bias, void* y, int x_
 // (the caller runs k_fused MD 1).  op = tap column class at padding 1 ((off + 1) & 1).
 int fconv4_try(const void* x, const float* k, const float* bias, void* y, int x_dtype, int y_dtype,
                int64_t batch, int C, int O, int G, int64_t h, int64_t w, int op, hipStream_t st) {
-    if (env_is("HYGRID_FCONV4", "0")) return HG_EUNSUP;   // A/B switch: the 2-column kernel
+    // Opt-in (HYGRID_FCONV4=1): at 18-row bands 1.7 % SLOWER than k_fused MD 1 on the 4K bf16
+    // b128 conv (2.710 vs 2.664 ms, profiles/r05/fconv4_ab.txt); bit-identical to it.
+    if (!env_is("HYGRID_FCONV4", "1")) return HG_EUNSUP;
     if (x_dtype != HG_BF16 || y_dtype != HG_BF16 || C != 3 || O != 3 || G != 1) return HG_EUNSUP;
     if ((w % 4) || w < 4 || h < 1 || batch < 1) return HG_EUNSUP;
     if (3 * h * w * 2 >= ((int64_t)1 << 31)) return HG_EUNSUP;   // 32-bit offsets per image

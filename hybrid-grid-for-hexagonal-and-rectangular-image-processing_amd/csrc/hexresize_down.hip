@@ -301,6 +301,9 @@ __global__ __launch_bounds__(HD_THREADS, HD_WPE) void k_hexresize_down(const Tin
     }
 }
 
+#ifndef HD_CPP
+#define HD_CPP 48           // planes per unit in the one-wave-per-unit grid (round 5)
+#endif
 template <typename Tin, typename Tout, int K, int DB, int P, bool SEP>
 static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st) {
     // resident waves: 256 CUs x 4 SIMDs x 4 waves; units split into plane chunks until
@@ -313,6 +316,11 @@ static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st)
     const int64_t upw = ue ? std::max(1, atoi(ue)) : 1;
     const int64_t tiles = (int64_t)D.nwin * D.nband;
     int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, (upw * RESIDENT + tiles - 1) / tiles));
+    // Round 5: one wave per unit and ~HD_CPP planes per unit (the records amortised over more
+    // planes; fewer, longer-lived units contend less): 4K -> 2K bf16 b32 0.496 -> 0.429 ms, 8K ->
+    // 4K fp16 b8 -1.9 % (profiles/r05/hexresize_grid_ab.txt).  HYGRID_TSK_GRID=0: the old rule.
+    const bool grid = !env_is("HYGRID_TSK_GRID", "0");
+    if (grid) nchunk = std::max<int64_t>(1, D.planes / HD_CPP);
     if (const char* e = getenv("HYGRID_TSK_CHUNKS"))   // A/B switch: plane chunks per tile
         nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, atoi(e)));
     // a chunk's planes are one buffer each way: 32-bit offsets, including the planes past
@@ -324,7 +332,7 @@ static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st)
     D.nchunk = (int)((D.planes + D.pc - 1) / D.pc);
     D.units = tiles * D.nchunk;
     int64_t waves = std::min<int64_t>(D.units, RESIDENT);
-    if (env_is("HYGRID_TSK_GRID", "1")) waves = std::min<int64_t>(D.units, (int64_t)1 << 30);   // A/B: a wave per unit
+    if (grid) waves = std::min<int64_t>(D.units, (int64_t)1 << 30);   // a wave per unit
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     hipLaunchKernelGGL((k_hexresize_down<Tin, Tout, K, DB, P, SEP>), dim3(blocks), dim3(HD_THREADS), 0, st,
                        (const Tin*)src, (Tout*)dst, D);

@@ -374,7 +374,8 @@ static int tu_launch(const void* src, void* dst, TriUpGeom& D, hipStream_t st) {
     const int64_t tiles = (int64_t)D.nwin * D.nband;
     int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, (RESIDENT + tiles / 2) / tiles));
     bool grid = false;
-    if (!env_is("HYGRID_TU_GRID", "0") && D.planes >= 2 * TU_CPP) {
+    // ('linear' only: 'nearest' u8 ran 0.407 -> 0.789 ms with it, profiles/r05/triup_grid_ab.txt)
+    if (!NEAR && !env_is("HYGRID_TU_GRID", "0") && D.planes >= 2 * TU_CPP) {
         nchunk = std::max<int64_t>(nchunk, D.planes / TU_CPP);
         grid = true;
     }

@@ -15,7 +15,10 @@ base=$(basename "$SRC" .hip)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize "$@" \
     -I"$PKG/csrc" -c "$PKG/csrc/$SRC" -o "$OBJ/variants/${base}_$NAME.o"
 objs=()
-for o in abi pipeline fused fused4 rt4; do
+# FULL=1: every object of the library (for entry points outside the fused pipeline, e.g. the conv)
+list="abi pipeline fused fused4 rt4"
+[ "${FULL:-0}" = 1 ] && list=$(cd "$OBJ" && ls *.o | sed 's/\.o$//')
+for o in $list; do
     if [ "$o" = "$base" ]; then objs+=("$OBJ/variants/${base}_$NAME.o"); else objs+=("$OBJ/$o.o"); fi
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$OUT/libhygrid_$NAME.so" "${objs[@]}"
