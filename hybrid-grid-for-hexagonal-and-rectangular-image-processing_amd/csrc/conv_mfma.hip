@@ -396,8 +396,14 @@ __device__ __forceinline__ void cd_wait_vm() {
 // LDS -> 2 workgroups per CU) or single-buffered (the DMA of chunk i + 1 is issued once chunk i's
 // MFMAs are done and waited for at the top of the next chunk; 47 KB -> 3 workgroups per CU, whose
 // MFMAs cover each other's waits)
-template <typename Tout, int NOT, bool WDB>
-__global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
+// NQT: 16-column tiles per workgroup (4; 3 with PSB1 = one raw-P buffer is the 4-waves-per-SIMD
+// build: 48 accumulators and <= 40 KB of LDS, so four workgroups fit a CU; round 5)
+#ifndef CD_WPE3
+#define CD_WPE3 4                     // waves per SIMD asked of the allocator for the NQT 3 build
+#endif
+template <typename Tout, int NOT, bool WDB, int NQT = 4, bool PSB1 = false>
+__global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(NQT == 3 ? CD_WPE3 : 1)))
+void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
                                                                    const cm_u4* __restrict__ wf,
                                                                    const int* __restrict__ flag,
                                                                    const float* __restrict__ bias,
@@ -411,7 +417,9 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
     static_assert(WPC % 4 == 0, "pieces");
     // one LDS array (so the DMA's M0 bases come from it): [psb | wsb x 2 | praw x 2]
     constexpr int LPSB = CB_PSZ * 16, LWSB = WSZ * 16, LPRAW = CD_PRAW * 4, NWB = WDB ? 2 : 1;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[LPSB + NWB * LWSB + 2 * LPRAW];
+    constexpr int NPB = PSB1 ? 1 : 2;                     // raw P buffers
+    constexpr int TQ = 16 * NQT;                          // output columns of this workgroup
+    __shared__ __attribute__((aligned(16))) unsigned char lds[LPSB + NWB * LWSB + NPB * LPRAW];
     cm_u4* const psb = reinterpret_cast<cm_u4*>(lds);
     const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -421,7 +429,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
     const int tr = (int)(bid % G.ntr); bid /= G.ntr;
     const int to = (int)(bid % G.nto);
     const int64_t b = bid / G.nto;
-    const int q0 = tq * CM_Q, r0 = tr * CM_ROWS, o0 = to * CM_O;
+    const int q0 = tq * TQ, r0 = tr * CM_ROWS, o0 = to * CM_O;
     const int r = r0 + wv;
     const int par = r & 1;
     const int Wp = G.w + 2 * G.p, Hp = G.h + 2 * G.p;
@@ -434,7 +442,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
                           px0 + CB_PP - 1 < G.w && q0 + G.mink + CB_PP - 1 < Wp;
     const int xs = px0 & ~1, sh = px0 - xs;               // dword-aligned raw start, shift
 
-    cm_f4 acc[NOT][4];
+    cm_f4 acc[NOT][NQT];
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot) {
 #pragma unroll
@@ -442,7 +450,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
             const int o = o0 + ot * 16 + lg * 4 + v;
             const float bv = (bias && o < G.O) ? bias[o] : 0.f;
 #pragma unroll
-            for (int qt = 0; qt < 4; ++qt) acc[ot][qt][v] = bv;
+            for (int qt = 0; qt < NQT; ++qt) acc[ot][qt][v] = bv;
         }
     }
     if (tid == 0) psb[CB_PSZ - 1] = cm_u4{0u, 0u, 0u, 0u};
@@ -477,7 +485,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
         }
     };
     auto dma_p = [&](int ci) {                            // chunk ci's raw P rows -> buffer (ci & 1)
-        const int buf = ci & 1;
+        const int buf = PSB1 ? 0 : ci & 1;
         if (interior) {
             // P rows: pieces j = wv * PPW + i = (cc, pr); lanes 0-39 one dword each
 #pragma unroll
@@ -505,12 +513,15 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
     dma_w(0);
     dma_p(0);
     for (int ci = 0; ci < nch; ++ci) {
-        const int buf = ci & 1;
+        const int buf = PSB1 ? 0 : ci & 1;
         const int c0 = ci * CM_CC;
         // chunk ci's pieces are done once at most the ones issued after them are outstanding
         // (vmcnt counts them in issue order): double-buffered, W(ci+1) and P(ci+1); single,
-        // only P(ci+1) (W(ci) was issued at the end of chunk ci-1, before P(ci+1))
-        if (ci + 1 < nch) {
+        // only P(ci+1) (W(ci) was issued at the end of chunk ci-1, before P(ci+1)).  PSB1: P(ci+1)
+        // is issued after this chunk's repack (one raw buffer), so everything issued is waited for
+        if (PSB1) {
+            cd_wait_vm<0>();
+        } else if (ci + 1 < nch) {
             if constexpr (WDB) {
                 dma_w(ci + 1);
                 dma_p(ci + 1);
@@ -534,7 +545,13 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
                 psb[f] = cm_u4{v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
                                v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16)};
             }
-        } else if (tid < 3 * CB_PP) {                     // the register staging (padding rules)
+        }
+        if (PSB1 && interior && ci + 1 < nch) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);           // this wave's repack reads are done
+            __builtin_amdgcn_s_barrier();                 // ... and every wave's: the raw buffer is free
+            dma_p(ci + 1);
+        }
+        if (!interior && tid < 3 * CB_PP) {               // the register staging (padding rules)
             const int pc = tid % CB_PP, ph = tid / CB_PP;
             const int px = q0 + G.mink + pc;
             const bool zc = px >= Wp;
@@ -561,13 +578,13 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
         for (int ot = 0; ot < NOT; ++ot) nparts |= flag[ci * (Opad / 16) + o0 / 16 + ot] ? 3 : 1;
         __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): this wave's LDS writes
         __builtin_amdgcn_s_barrier();                     // psb and the weights complete
-        // ---- 2 k blocks x 4 column tiles x 3 weight parts x NOT channel tiles -------------
-        const cm_u4* const wsb = reinterpret_cast<const cm_u4*>(lds + LPSB + (WDB ? buf : 0) * LWSB);
+        // ---- 2 k blocks x NQT column tiles x 3 weight parts x NOT channel tiles -----------
+        const cm_u4* const wsb = reinterpret_cast<const cm_u4*>(lds + LPSB + (WDB ? (ci & 1) : 0) * LWSB);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-            cm_b8 bf[4];
+            cm_b8 bf[NQT];
 #pragma unroll
-            for (int qt = 0; qt < 4; ++qt)
+            for (int qt = 0; qt < NQT; ++qt)
                 bf[qt] = __builtin_bit_cast(cm_b8, psb[pidx[kb] < 0 ? CB_PSZ - 1 : pidx[kb] + qt * 16]);
 #pragma unroll
             for (int pt = 0; pt < 3; ++pt) {
@@ -576,7 +593,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
                 for (int ot = 0; ot < NOT; ++ot) {
                     const cm_b8 af = __builtin_bit_cast(cm_b8, wsb[((pt * 2 + kb) * CM_O + ot * 16 + li) * 4 + cd_wslot(li, lg)]);
 #pragma unroll
-                    for (int qt = 0; qt < 4; ++qt)
+                    for (int qt = 0; qt < NQT; ++qt)
                         acc[ot][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[qt], acc[ot][qt], 0, 0, 0);
                 }
             }
@@ -597,7 +614,7 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma_bf16d(const __bf16*
             const int o = o0 + ot * 16 + lg * 4 + v;
             if (o >= G.O) continue;
 #pragma unroll
-            for (int qt = 0; qt < 4; ++qt) {
+            for (int qt = 0; qt < NQT; ++qt) {
                 const int q = q0 + qt * 16 + li;
                 if (q >= G.wo) continue;
                 float val = acc[ot][qt][v];
@@ -666,6 +683,21 @@ int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_
             hipLaunchKernelGGL(k_wsplit_bf16, dim3(nch, Opad / 16), dim3(128), 0, st, k, wfr, flg, G.C, G.O, Opad);
             // weight chunks single-buffered (A/B switch HYGRID_CONV_WDB=1: double-buffered)
             const bool wdb = env_is("HYGRID_CONV_WDB", "1");
+            // HYGRID_CONV_NQT=3: 3 column tiles per workgroup and one raw-P buffer (4 waves/SIMD)
+            if (nt == 4 && !wdb && env_is("HYGRID_CONV_NQT", "3")) {
+                G.ntq = (G.wo + 48 - 1) / 48;
+                const int64_t blocks3 = B * (int64_t)G.ntq * G.ntr * G.nto;
+                if (blocks3 > INT_MAX) { (void)hipFreeAsync(ws, st); return HG_EUNSUP; }
+                if (y_dtype == HG_BF16)
+                    hipLaunchKernelGGL((k_hexconv_mfma_bf16d<__bf16, 4, false, 3, true>), dim3((unsigned)blocks3), blk, 0, st,
+                                       (const __bf16*)x, wfr, flg, b, (__bf16*)y, G, Opad);
+                else
+                    hipLaunchKernelGGL((k_hexconv_mfma_bf16d<float, 4, false, 3, true>), dim3((unsigned)blocks3), blk, 0, st,
+                                       (const __bf16*)x, wfr, flg, b, (float*)y, G, Opad);
+                const int ls3 = launch_status();
+                const hipError_t fe3 = hipFreeAsync(ws, st);
+                return ls3 != HG_OK ? ls3 : (int)fe3;
+            }
 #define HG_CD_LAUNCH2(TO, NT_, WDB_)                                                          \
             hipLaunchKernelGGL((k_hexconv_mfma_bf16d<TO, NT_, WDB_>), grid, blk, 0, st, (const __bf16*)x, wfr, flg, b, (TO*)y, G, Opad);
 #define HG_CD_LAUNCH(TO)                                                                      \

@@ -96,9 +96,13 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     const int ngrp = (F.nwin + F4_GW - 1) / F4_GW;
     // block -> (window group, band, image): group fastest (F4_ORDER 0) or band fastest (1: the
     // bands of one window group run side by side, sharing their 4 halo rows in L2)
-    const int grp = (int)(F4_ORDER ? (blk / F.nband) % ngrp : blk % ngrp);
-    const int band = (int)(F4_ORDER ? blk % F.nband : (blk / ngrp) % F.nband);
-    const int64_t b = blk / ((int64_t)ngrp * F.nband);
+    // (2: group fastest, then image, then band: the waves resident together walk the same
+    // rows of many images)
+    const int grp = (int)(F4_ORDER == 1 ? (blk / F.nband) % ngrp : blk % ngrp);
+    const int band = (int)(F4_ORDER == 1 ? blk % F.nband
+                           : F4_ORDER == 2 ? blk / ((int64_t)ngrp * F.B) : (blk / ngrp) % F.nband);
+    const int64_t b = F4_ORDER == 2 ? (blk / ngrp) % F.B : blk / ((int64_t)ngrp * F.nband);
+    if (band >= F.nband) return;
     if (b >= F.B) return;                            // uniform per workgroup
     const int win = grp * F4_GW + wslot;             // may be >= nwin: runs, owns nothing
     const int W0 = win * F4_OWN - F4_HL;

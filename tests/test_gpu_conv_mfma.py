@@ -267,12 +267,14 @@ def test_mfma_bf16_dma_bit_identical_to_register_staging(case, pad, off):
 
 
 @pytest.mark.parametrize("case", DMA_CASES)
-@pytest.mark.parametrize("env", [("HYGRID_CONV_WDB", "1"), ("HYGRID_CONV_NT", "2")])
+@pytest.mark.parametrize("env", [("HYGRID_CONV_WDB", "1"), ("HYGRID_CONV_NT", "2"),
+                                 ("HYGRID_CONV_NQT", "3")])
 def test_mfma_bf16_dma_weight_buffering_and_tiles_bit_identical(case, env):
     """The single-buffered weight chunks (default) and the double-buffered ones
     (HYGRID_CONV_WDB=1) stage the same fragments for the same MFMAs: bit-identical outputs; two
     output-channel tiles per workgroup (HYGRID_CONV_NT=2) compute each output's sum in the same
-    order: bit-identical too."""
+    order: bit-identical too; so do three 16-column tiles per workgroup with one raw-P buffer
+    (HYGRID_CONV_NQT=3, the 4-waves-per-SIMD build)."""
     B, C, O_, h, w = case
     k, b = _weights(O_, C, h * 3 + w)
     x = _bf16_input((B, C, h, w), h + 2 * w)
