@@ -128,6 +128,11 @@ static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
                                       // conv rows in LDS (3 ds_read_b32 per channel at per-lane
                                       // addresses) instead of 5 DPP moves + 9 selects per channel
 #endif
+#ifndef FU_PTAB
+#define FU_PTAB 1                     // MD 3 / 4 / 5: the output rows' uniform lattice terms (0.5 i_,
+                                      // i_f, i_n) from a per-band LDS table instead of fp64 VALU per
+                                      // output row; weights selected before subtracting (round 5)
+#endif
 #ifndef FU_DMA
 #define FU_DMA 0                      // MD 0, 16-bit input: rect rows arrive by LDS-DMA as
                                       // workgroup-wide 1-KiB row pieces (one per plane, issued by
@@ -387,6 +392,11 @@ void k_fused(const Tin* __restrict__ x,
     constexpr bool PLDS = FU_PLDS && PYR;
     constexpr int ZW = 130;
     __shared__ float zl_all[PLDS ? GW : 1][PLDS ? 2 * O * ZW : 1];
+    // PTAB: per output row of the band {0.5 i_, i_f} and i_n (geometry_np.py:601-612)
+    constexpr bool PTAB = FU_PTAB && PYR;
+    constexpr int NPT = FU_RB_PYR / 2 + 1;
+    __shared__ double ptd_all[PTAB ? GW : 1][PTAB ? NPT : 1][2];
+    __shared__ int pti_all[PTAB ? GW : 1][PTAB ? NPT : 1];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4* lut = DMA ? reinterpret_cast<float4*>(dsm) + wslot * FU_LUT : lut_all[DMA ? 0 : wslot];
@@ -482,6 +492,18 @@ void k_fused(const Tin* __restrict__ x,
     const double t_yv = PYR ? axis_at(F.tys, min(max(bo, 0), F.w2 - 1)) : 0.0;
     const double t_cw = ((double)F.w1 - 0.5) * 0.5;
     const double t_ch = (double)(F.h1 - 1) * 0.5;
+    if constexpr (PTAB) {
+        for (int e = lane; e < NPT; e += 64) {
+            const int a = (s0 >> 1) + e;
+            const double i_ = axis_at(F.txs, min(a, F.h2 - 1)) + t_ch;   // :601 (uniform per row)
+            const int i_n = (int)i_;
+            ptd_all[wslot][e][0] = 0.5 * i_;
+            ptd_all[wslot][e][1] = i_ - (double)(float)i_n;
+            pti_all[wslot][e] = i_n;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
     // staging slot of this lane's two output columns (non-owned lanes write a pad dword)
     const int sidx = (lane >= FU_HL / 2 && lane < (FU_HL + FU_OWN) / 2)
                          ? wslot * (FU_OWN / 2) + lane - FU_HL / 2 : GDW + (lane & 3);
@@ -833,16 +855,29 @@ void k_fused(const Tin* __restrict__ x,
         // lattice's (i, j) index frame (an affine image of the reference's Cartesian frame,
         // :651-678): (1 - i_f, i_f - j_f, j_f) if i_f > j_f, else (1 - j_f, j_f - i_f, i_f).
         auto pyr_out = [&](const fu_f2 (&Z1)[O], int a) {
-            const double i_ = axis_at(F.txs, a) + t_ch;                  // uniform
-            const int i_n = __builtin_amdgcn_readfirstlane((int)i_);
+            double hi, i_f;
+            int i_n;
+            if constexpr (PTAB) {                                       // the band's table (uniform)
+                const int e = a - (s0 >> 1);
+                hi = ptd_all[wslot][e][0];
+                i_f = ptd_all[wslot][e][1];
+                i_n = __builtin_amdgcn_readfirstlane(pti_all[wslot][e]);
+            } else {
+                const double i_ = axis_at(F.txs, a) + t_ch;              // uniform
+                i_n = __builtin_amdgcn_readfirstlane((int)i_);
+                i_f = i_ - (double)(float)i_n;
+                hi = 0.5 * i_;
+            }
             const bool e1 = i_n != 2 * a;                                // uniform
-            const double i_f = i_ - (double)(float)i_n;
-            const double j_ = 0.5 * i_ + t_yv + t_cw;
+            const double j_ = hi + t_yv + t_cw;                          // = 0.5 * i_ + y_ + cw (:602)
             const int j_n = (int)j_;
             const double j_f = j_ - (double)(float)j_n;
             const bool flag = i_f > j_f;
-            const float wa = (float)(flag ? 1.0 - i_f : 1.0 - j_f);
-            const float wb = (float)(flag ? i_f - j_f : j_f - i_f);
+            // the same values as (flag ? 1 - i_f : 1 - j_f) and (flag ? i_f - j_f : j_f - i_f):
+            // select first, subtract once (IEEE subtraction is sign-symmetric)
+            const double d_ = i_f - j_f;
+            const float wa = (float)(1.0 - (flag ? i_f : j_f));
+            const float wb = (float)(flag ? d_ : -d_);
             const float wg = (float)(flag ? j_f : i_f);
             const int c0 = j_n - (i_n + 1) / 2, c1 = j_n - (i_n + 2) / 2;
             const int d0 = c0 - 2 * bo, d1 = c1 - 2 * bo;
