@@ -45,6 +45,12 @@ namespace hg {
                                        // steps ahead, no VGPRs, no workgroup barrier) instead of
                                        // the register ring
 #endif
+#ifndef F4_SAUX
+#define F4_SAUX 0                      // cache-policy bits of the output stores (A/B: 2 nt, 16 sc1)
+#endif
+#ifndef F4_LAUX
+#define F4_LAUX 0                      // ... of the rect-row loads
+#endif
 #ifndef F4_NOMEM
 #define F4_NOMEM 0                     // diagnostic floor: every row load / store hits row 0 of its
                                        // plane (cache-resident), the arithmetic unchanged (1: loads
@@ -277,7 +283,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             constexpr int SL = decltype(SLc)::value;
             const unsigned so = row_off(k);
 #pragma unroll
-            for (int c = 0; c < C; ++c) raw[SL][c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, xoff, so + c * xplane, 0);
+            for (int c = 0; c < C; ++c) raw[SL][c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, xoff, so + c * xplane, F4_LAUX);
         };
         auto convert = [&](auto RSc, auto XSc) {
             constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
@@ -403,7 +409,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
                 typedef __bf16 t2v __attribute__((ext_vector_type(2)));
                 const f4_u2 v = {__builtin_bit_cast(unsigned, t2v{(__bf16)o0, (__bf16)o1}),
                                  __builtin_bit_cast(unsigned, t2v{(__bf16)o2, (__bf16)o3})};
-                __builtin_amdgcn_raw_buffer_store_b64(v, yrs, yoff, so + o * yplane, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(v, yrs, yoff, so + o * yplane, F4_SAUX);
             }
         };
 
