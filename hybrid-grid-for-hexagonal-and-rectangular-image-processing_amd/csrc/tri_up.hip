@@ -66,6 +66,9 @@ namespace hg {
 #ifndef TU_PDP_VLD
 #define TU_PDP_VLD 4        // with TU_VLD: planes of rows held in VGPRs ahead of the one blended
 #endif
+#ifndef TU_NKMUL
+#define TU_NKMUL 1          // 'nearest' 8-bit: output columns per lane x this (A/B: 2 -> 8-B stores)
+#endif
 #ifndef TU_CPP
 #define TU_CPP 24           // planes per unit when the grid has a wave per unit (round 5)
 #endif
@@ -433,7 +436,8 @@ int triup_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t plan
     // K output columns per lane: the natural width (one dword of input samples per lane:
     // 8 / 4 / 2 for 1 / 2 / 4-byte inputs; stores of <= 16 B), or one column when that window
     // of 64 K columns does not keep its vertices in the WC input columns or K does not divide w1
-    const int wc = TU_PCB / E, kn = std::max(1, (E == 1 ? 8 : E == 2 ? 4 : 2) / (near_ ? 2 : 1) / TU_KDIV);
+    const int wc = TU_PCB / E, kn = std::max(1, (E == 1 ? 8 : E == 2 ? 4 : 2) / (near_ ? 2 : 1) / TU_KDIV) *
+                                    (near_ && E == 1 ? TU_NKMUL : 1);
     int K = 0;
     for (const int k : {kn, 1})
         if (!K && w1 % k == 0 && tsk_lattice_ok(g, 64 * k, wc, 4 / E, D.qmin, qmax)) K = k;
@@ -447,7 +451,7 @@ int triup_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t plan
 #define HG_TU_K(TI, TO, KN, NR_)                                                                \
     return K == 1 ? tu_launch<TI, TO, 1, NR_>(src, dst, D, st) : tu_launch<TI, TO, KN, NR_>(src, dst, D, st);
     if (near_) {
-        if (E == 1) { HG_TU_K(uint8_t, uint8_t, 4 / TU_KDIV, true) }
+        if (E == 1) { HG_TU_K(uint8_t, uint8_t, 4 * TU_NKMUL / TU_KDIV, true) }
         if (E == 2) { HG_TU_K(unsigned short, unsigned short, (2 / TU_KDIV > 0 ? 2 / TU_KDIV : 1), true) }
         HG_TU_K(unsigned, unsigned, 1, true)
     }
