@@ -133,6 +133,10 @@ static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
                                       // i_f, i_n) from a per-band LDS table instead of fp64 VALU per
                                       // output row; weights selected before subtracting (round 5)
 #endif
+#ifndef FU_PCOLINT
+#define FU_PCOLINT 1                  // MD 3 / 4 / 5: windows whose owned vertices are all inside the
+                                      // raster skip the per-vertex column tests (round 5)
+#endif
 #ifndef FU_DMA
 #define FU_DMA 0                      // MD 0, 16-bit input: rect rows arrive by LDS-DMA as
                                       // workgroup-wide 1-KiB row pieces (one per plane, issued by
@@ -490,6 +494,9 @@ void k_fused(const Tin* __restrict__ x,
     // PYR: per-lane hexresize lattice constants (geometry_np.py:570-602) on the conv image
     // (h1, w1): j_ = 0.5 i_ + y_(b) + (w1 - 0.5) / 2 per output row
     const double t_yv = PYR ? axis_at(F.tys, min(max(bo, 0), F.w2 - 1)) : 0.0;
+    // PYR: every owned lane's triangle vertices (conv columns 2b - 2 .. 2b + 2, pf_lattice_ok)
+    // inside the raster: the window needs no column validity tests (uniform; round 5)
+    const bool pcolint = PYR && FU_PCOLINT && W0 >= -2 && W0 + 124 < F.w1;
     const double t_cw = ((double)F.w1 - 0.5) * 0.5;
     const double t_ch = (double)(F.h1 - 1) * 0.5;
     if constexpr (PTAB) {
@@ -897,10 +904,19 @@ void k_fused(const Tin* __restrict__ x,
                 __builtin_amdgcn_wave_barrier();
                 asm volatile("" ::: "memory");
                 const int r0b = e1 ? O * ZW : 0;
-                auto col = [&](int c) { return min(max(c - W0, 0), 127); };
-                const int a1 = v1 ? r0b + col(c0) : 128;
-                const int a2 = v2 ? (flag ? O * ZW + col(c1) : r0b + col(c0 + 1)) : 128;
-                const int a3 = v3 ? O * ZW + col(c1 + 1) : 128;
+                int a1, a2, a3;
+                if (pcolint) {
+                    // owned lanes' vertices are inside; halo lanes (outputs dropped) may read
+                    // past their window's row (other LDS data or zeros beyond the allocation)
+                    a1 = r0b + c0 - W0;
+                    a2 = flag ? (r1in ? O * ZW + c1 - W0 : 128) : r0b + c0 + 1 - W0;
+                    a3 = r1in ? O * ZW + c1 + 1 - W0 : 128;
+                } else {
+                    auto col = [&](int c) { return min(max(c - W0, 0), 127); };
+                    a1 = v1 ? r0b + col(c0) : 128;
+                    a2 = v2 ? (flag ? O * ZW + col(c1) : r0b + col(c0 + 1)) : 128;
+                    a3 = v3 ? O * ZW + col(c1 + 1) : 128;
+                }
     #pragma unroll
                 for (int o = 0; o < O; ++o) {
                     const float q1 = zl[a1 + o * ZW], q2 = zl[a2 + o * ZW], q3 = zl[a3 + o * ZW];
