@@ -133,6 +133,15 @@ static_assert(FU_OWN % 2 == 0 && FU_HL % 2 == 0 && FU_HL + FU_OWN <= 128 - 2,
                                       // i_f, i_n) from a per-band LDS table instead of fp64 VALU per
                                       // output row; weights selected before subtracting (round 5)
 #endif
+#ifndef FU_FMIX
+#define FU_FMIX 0                     // MD 3, fp16 input: the r2h vertical blend as v_fma_mix_f32 on the
+                                      // raw f16 rows (no conversion pass; the same products and sums):
+                                      // 118 -> 96 VGPRs, 5 waves per SIMD, but level 0 within 0.7 %
+                                      // (profiles/r05/pyramid_fmix_ab.txt): off
+#endif
+#ifndef FU_WPE_FMIX
+#define FU_WPE_FMIX 5                 // MD 3 with FMIX: the raw f16 ring leaves room for a 5th wave
+#endif
 #ifndef FU_PCOLINT
 #define FU_PCOLINT 1                  // MD 3 / 4 / 5: windows whose owned vertices are all inside the
                                       // raster skip the per-vertex column tests (round 5)
@@ -319,6 +328,15 @@ __device__ __forceinline__ void fu_h2r3_odd(float& e0, float& o0, float& e1, flo
         : "v"(c13), "v"(wp));
     o0 = a0; o1 = a1; o2 = a2;
 }
+// d = a * f16(half HI of b) + c in fp32 (v_fma_mix_f32: the f16 operand converts exactly, one
+// rounding: the same value as fmaf(a, (float)h, c))
+template <int HI>
+__device__ __forceinline__ float fu_fmix(float a, unsigned b, float c) {
+    float d;
+    if constexpr (HI) asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 template <typename T>
 __device__ __forceinline__ fu_f2 fu_unpack2(typename RawOf<T>::type r, unsigned hi16) {
     float e, o;
@@ -349,7 +367,8 @@ template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD = 0>
 // MD 1 with 16-bit input and output fits 128 VGPRs (4 waves per SIMD); an fp32 raw ring or
 // fp32 stores need more, and capping those at 128 spills to scratch inside the row loop.
 __global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(
-    (MD == 1 && sizeof(Tin) == 2 && sizeof(Tout) == 2) ? FU_WPE_CONV : FU_WPE)))
+    (MD == 1 && sizeof(Tin) == 2 && sizeof(Tout) == 2) ? FU_WPE_CONV
+    : (MD == 3 && FU_FMIX && std::is_same<Tin, _Float16>::value) ? FU_WPE_FMIX : FU_WPE)))
 void k_fused(const Tin* __restrict__ x,
                                                       const float* __restrict__ kern,
                                                       const float* __restrict__ bias,
@@ -623,6 +642,15 @@ void k_fused(const Tin* __restrict__ x,
         Raw raw[6][C];                      // rect rows in flight, slot (row - s0) % 6
         Raw rawn[C];                        // DMA: the next rect row, read from the LDS ring
         fu_f2 XP[3][C];                     // rect rows as f32 (even, odd) pairs, slot (row - s0) % 3
+        // FMIX: the rect rows stay raw (two f16 per lane) and the vertical blend reads them with
+        // v_fma_mix_f32 (MD 3 from an fp16 rect image, register ring only)
+        constexpr bool FMIX = FU_FMIX && MD == 3 && !DMA && std::is_same<Tin, _Float16>::value;
+        Raw XR[3][C];
+        auto xset = [&](auto XSc, int c, Raw r) {
+            constexpr int XS = decltype(XSc)::value;
+            if constexpr (FMIX) XR[XS][c] = r;
+            else XP[XS][c] = fu_unpack2<Tin>(r, hi16);
+        };
         float ZE[3][O], ZO[3][O];           // conv rows being accumulated, slot (row - s0) % 3
         constexpr bool PK = FU_PK && MD != 2;
         static_assert(PK || !PYR, "the pyramid modes use the packed stencil");
@@ -638,7 +666,7 @@ void k_fused(const Tin* __restrict__ x,
         auto convert = [&](auto RSc, auto XSc) {
             constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
     #pragma unroll
-            for (int c = 0; c < C; ++c) XP[XS][c] = fu_unpack2<Tin>(raw[RS][c], hi16);
+            for (int c = 0; c < C; ++c) xset(IC<XS>{}, c, raw[RS][c]);
         };
         // DMA: rect row R lives in ring slot (R - s0 + 2) % NSR; waves 0 .. C-1 each move one
         // plane's 1-KiB piece of it (uniform branch), every wave reads its column pair
@@ -713,7 +741,21 @@ void k_fused(const Tin* __restrict__ x,
     #pragma unroll
             for (int c = 0; c < C; ++c) {
                 float ve, vo;
-                if constexpr (VPK) {                // the same products and sums, packed
+                if constexpr (FMIX) {               // the same products and sums on the raw f16 rows
+                    float m0 = -0.f;                // x * y + (-0) = x * y exactly (signed zeros too)
+                    asm volatile("" : "+v"(m0));
+                    const Raw r0 = XR[S0][c], r1 = XR[S1][c], r2 = XR[S2][c];
+                    if constexpr (RC == 1) {
+                        ve = fu_fmix<0>(L.y, r1, fu_fmix<0>(L.x, r0, m0));
+                        vo = fu_fmix<1>(L.y, r1, fu_fmix<1>(L.x, r0, m0));
+                    } else if constexpr (RC == 2) {
+                        ve = fu_fmix<0>(L.z, r2, fu_fmix<0>(L.y, r1, m0));
+                        vo = fu_fmix<1>(L.z, r2, fu_fmix<1>(L.y, r1, m0));
+                    } else {
+                        ve = fu_fmix<0>(L.z, r2, fu_fmix<0>(L.y, r1, fu_fmix<0>(L.x, r0, m0)));
+                        vo = fu_fmix<1>(L.z, r2, fu_fmix<1>(L.y, r1, fu_fmix<1>(L.x, r0, m0)));
+                    }
+                } else if constexpr (VPK) {         // the same products and sums, packed
                     const fu_f2 Lxy = {L.x, L.y}, Lzw = {L.z, L.w};
                     fu_f2 V;
                     if constexpr (RC == 1) {
@@ -1100,9 +1142,9 @@ void k_fused(const Tin* __restrict__ x,
             }
     #pragma unroll
             for (int c = 0; c < C; ++c) {
-                XP[1][c] = fu_unpack2<Tin>(t0[c], hi16);   // row s0-2 -> slot 1
-                XP[2][c] = fu_unpack2<Tin>(t1[c], hi16);   // row s0-1 -> slot 2
-                XP[0][c] = fu_unpack2<Tin>(t2[c], hi16);   // row s0   -> slot 0
+                xset(IC<1>{}, c, t0[c]);   // row s0-2 -> slot 1
+                xset(IC<2>{}, c, t1[c]);   // row s0-1 -> slot 2
+                xset(IC<0>{}, c, t2[c]);   // row s0   -> slot 0
             }
         }
         urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});   // u row s0-1: above only
