@@ -51,6 +51,11 @@ namespace hg {
 #ifndef F4_LAUX
 #define F4_LAUX 0                      // ... of the rect-row loads
 #endif
+#ifndef F4_DIAG_NOBEL
+#define F4_DIAG_NOBEL 0                // diagnostic (wrong results): skip the stencil's 'below' taps
+                                       // (36 of 132 packed FMAs per step) to test whether compute and
+                                       // memory time add or overlap
+#endif
 #ifndef F4_NOMEM
 #define F4_NOMEM 0                     // diagnostic floor: every row load / store hits row 0 of its
                                        // plane (cache-resident), the arithmetic unchanged (1: loads
@@ -375,7 +380,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
                         tapk(IC<3>{}, ZA[S1][o], ZB[S1][o], PC);
                         tapk(IC<4>{}, ZA[S1][o], ZB[S1][o], PC);
                     }
-                    if constexpr (BEL) {
+                    if constexpr (BEL && !F4_DIAG_NOBEL) {
                         tapk(IC<5>{}, ZA[S0][o], ZB[S0][o], PB);
                         tapk(IC<6>{}, ZA[S0][o], ZB[S0][o], PB);
                     }
