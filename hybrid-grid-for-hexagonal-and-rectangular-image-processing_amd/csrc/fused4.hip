@@ -56,6 +56,10 @@ namespace hg {
                                        // (36 of 132 packed FMAs per step) to test whether compute and
                                        // memory time add or overlap
 #endif
+#ifndef F4_DIAG_NOFP64
+#define F4_DIAG_NOFP64 0               // diagnostic (wrong results): row table and column weights
+                                       // from constants instead of the fp64 lattice (prologue cost)
+#endif
 #ifndef F4_NOMEM
 #define F4_NOMEM 0                     // diagnostic floor: every row load / store hits row 0 of its
                                        // plane (cache-resident), the arithmetic unchanged (1: loads
@@ -128,6 +132,8 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
         float4 t = {0.f, 0.f, 0.f, 0.f};
         if (UIN) {
             t.y = (r >= 0 && r < F.h) ? 1.f : 0.f;       // u row r = input row r; 0: padding row
+        } else if (F4_DIAG_NOFP64) {
+            t.x = 0.25f; t.y = 0.75f;
         } else if (r >= 0 && r < F.h1) {
             const double i_ = axis_at(F.rxs, r) + (double)(F.h - 1) * 0.5;   // :440
             const int in = (int)i_;                                          // :444
@@ -164,7 +170,9 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             float* wr = s ? wo[k] : we[k];
             wr[0] = wr[1] = wr[2] = 0.f;
             const int q = ce + 2 * k + s;
-            if (!UIN && q >= 0 && q < F.w1) {
+            if (F4_DIAG_NOFP64) {
+                wr[0] = 0.25f; wr[1] = 0.75f;
+            } else if (!UIN && q >= 0 && q < F.w1) {
                 const double j_ = axis_at(F.rys, q) + (double)(F.w - 1) * 0.5;   // :441
                 const int jn = (int)j_;
                 const double jf = j_ - (double)(float)jn;
