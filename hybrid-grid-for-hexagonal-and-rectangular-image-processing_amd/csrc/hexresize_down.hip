@@ -71,8 +71,10 @@ __device__ __forceinline__ void fu_static_for(F&& f) {
 #ifndef HD_P4
 #define HD_P4 2
 #endif
+// waves per SIMD asked of the register allocator: 4 capped the K = 4 kernels at 128 VGPRs
+// and spilled 124-180 B per lane; 3 waves without spills are 7-18 % faster (r05 A/B)
 #ifndef HD_WPE
-#define HD_WPE 4            // waves per SIMD asked of the register allocator
+#define HD_WPE 3
 #endif
 #ifndef HD_RING
 #define HD_RING 8576        // LDS ring bytes per wave
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(HD_THREADS, HD_WPE) void k_hexresize_down(const Tin
                 // one sample's fp64 temporaries at a time (interleaved samples spill)
                 __builtin_amdgcn_sched_barrier(0);
                 const int bb = b0 + P * lane + 64 * P * (kk / P) + kk % P;
-                const TriSample s = tri_sample(D.g, a, bb < bend ? bb : b0);
+                const TriSample s = tri_sample_fast(D.g, a, bb < bend ? bb : b0);   // (tri_fast_ok: host)
                 if (kk == 0) r0[k] = __builtin_amdgcn_readfirstlane((int)s.i_n);   // i_n: row only
                 auto ix = [&](int v) {                           // vertex v's ring index
                     return (s.vk >> v) & 1 ? min(max((int)s.c[v] - xb, 0), WC - 1) : WC;
@@ -357,6 +359,7 @@ int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t 
     if ((h * w * 2) * 4 >= ((int64_t)1 << 31) || (h1 * w1 * 4) * 4 >= ((int64_t)1 << 31))
         return HG_EUNSUP;
     const Geom g = make_tri(h, w, h1, w1, op == HG_OP_HEXRESIZE ? 0.5 : 0.75);
+    if (!tri_fast_ok(g)) return HG_EUNSUP;
     // input columns per output column: 512-column windows (16-B pieces) when downsampling,
     // 128-column windows (4-B pieces) when upsampling or the rows are not 16-B aligned; a
     // lane owns K output columns of its window in groups of P adjacent ones (K = 4, or

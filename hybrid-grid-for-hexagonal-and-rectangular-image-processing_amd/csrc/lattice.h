@@ -113,19 +113,24 @@ struct TriSample {
 // (h, w) = (g.h, g.w).  Shared by hex->rect / hexresize (x_, y_ from linspace axes) and
 // image_geometric_transformation (x_, y_ from an inverse homography, geometry_np.py:107-187,
 // whose i_f = i_ - i_n equals the (float) cast below for |i_n| < 2^24).
-__host__ __device__ __forceinline__ TriSample tri_sample_xy(const Geom& g, double x_, double y_) {
+// I: the integer type of the lattice indices.  int64_t is the reference's astype(int);
+// int gives the same values whenever |i_|, |j_| < 2^31 (and the float casts below are exact
+// for |i_n|, |j_n| < 2^24 either way): tri_sample_fast, for the callers that check tri_fast_ok.
+template <typename I>
+__host__ __device__ __forceinline__ TriSample tri_sample_xy_t(const Geom& g, double x_, double y_) {
     TriSample s;
     const double hh = g.hh, ww = g.ww;
     double i_ = x_ + (double)(g.h - 1) * 0.5;            // :276
     double j_ = 0.5 * i_ + y_ + (ww - 0.5) * 0.5;        // :277
-    s.i_n = (int64_t)i_;
-    s.j_n = (int64_t)j_;
-    s.i_f = i_ - (double)(float)s.i_n;                   // :284-285
-    s.j_f = j_ - (double)(float)s.j_n;
-    int64_t s1 = (int64_t)((double)(s.i_n + 1) / 2.0);   // :289 true div, then trunc
-    int64_t s2 = (int64_t)((double)(s.i_n + 2) / 2.0);
-    int64_t ii[4] = {s.i_n, s.i_n + 1, s.i_n, s.i_n + 1};
-    int64_t jj[4] = {s.j_n - s1, s.j_n - s2, s.j_n + 1 - s1, s.j_n + 1 - s2};
+    const I in_ = (I)i_, jn_ = (I)j_;
+    s.i_n = in_;
+    s.j_n = jn_;
+    s.i_f = i_ - (double)(float)in_;                     // :284-285
+    s.j_f = j_ - (double)(float)jn_;
+    I s1 = (I)((double)(in_ + 1) / 2.0);                 // :289 true div, then trunc
+    I s2 = (I)((double)(in_ + 2) / 2.0);
+    I ii[4] = {in_, in_ + 1, in_, in_ + 1};
+    I jj[4] = {jn_ - s1, jn_ - s2, jn_ + 1 - s1, jn_ + 1 - s2};
     s.flag = s.i_f > s.j_f;                              // :298
     s.valid = 0;
 #pragma unroll
@@ -133,7 +138,7 @@ __host__ __device__ __forceinline__ TriSample tri_sample_xy(const Geom& g, doubl
         if (ii[k] >= 0 && jj[k] >= 0 && ii[k] < g.h && jj[k] < g.w) s.valid |= 1 << k;
     int k2 = s.flag ? 1 : 2;                             // :321-322
     s.r[0] = ii[0]; s.c[0] = jj[0];
-    s.r[1] = ii[k2]; s.c[1] = jj[k2];
+    s.r[1] = s.flag ? ii[1] : ii[2]; s.c[1] = s.flag ? jj[1] : jj[2];   // ii[k2] (selects: no scratch)
     s.r[2] = ii[3]; s.c[2] = jj[3];
     s.vk = (s.valid & 1) | (((s.valid >> k2) & 1) << 1) | (((s.valid >> 3) & 1) << 2);
     // cartesian vertices :326-331
@@ -163,8 +168,39 @@ __host__ __device__ __forceinline__ TriSample tri_sample_xy(const Geom& g, doubl
     return s;
 }
 
+__host__ __device__ __forceinline__ TriSample tri_sample_xy(const Geom& g, double x_, double y_) {
+    return tri_sample_xy_t<int64_t>(g, x_, y_);
+}
+
+// Vertex m of a sample by selects: s.r[m] with a run-time m puts the sample in scratch.
+__host__ __device__ __forceinline__ int64_t tri_pick_r(const TriSample& s, int m) {
+    return m == 0 ? s.r[0] : m == 1 ? s.r[1] : s.r[2];
+}
+__host__ __device__ __forceinline__ int64_t tri_pick_c(const TriSample& s, int m) {
+    return m == 0 ? s.c[0] : m == 1 ? s.c[1] : s.c[2];
+}
+
 __host__ __device__ __forceinline__ TriSample tri_sample(const Geom& g, int64_t a, int64_t b) {
     return tri_sample_xy(g, axis_at(g.xs, a), axis_at(g.ys, b));
+}
+
+// axis_at for an axis with n > 1 and step != 0: the same value without the (k / div) * delta
+// branch, whose fp64 division the compiler otherwise evaluates for every sample and selects away.
+__host__ __device__ __forceinline__ double axis_at_step(const Axis& a, int64_t k) {
+    if (k == a.n - 1) return a.stop;
+    const double y = (double)k * a.step;
+    return y + a.start;
+}
+
+// tri_sample bit for bit, cheaper (32-bit lattice indices, no speculated division) when
+// tri_fast_ok(g) holds (host-checked by the streaming kernels that compute per-sample records).
+inline bool tri_fast_ok(const Geom& g) {
+    const int64_t lim = (int64_t)1 << 22;   // |i_|, |j_| < 2^23 << 2^24
+    return g.xs.n > 1 && g.ys.n > 1 && g.xs.step != 0.0 && g.ys.step != 0.0 && g.h < lim &&
+           g.w < lim && g.h1 < lim && g.w1 < lim;
+}
+__host__ __device__ __forceinline__ TriSample tri_sample_fast(const Geom& g, int64_t a, int64_t b) {
+    return tri_sample_xy_t<int>(g, axis_at_step(g.xs, a), axis_at_step(g.ys, b));
 }
 
 }  // namespace hg

@@ -357,7 +357,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_resample_nearest(const E* __rest
         } else {
             TriSample s = tri_sample(g, a, b);
             const int m = s.argmin;
-            off[k] = ((s.vk >> m) & 1) ? (int)(s.r[m] * g.w + s.c[m]) : -1;
+            off[k] = ((s.vk >> m) & 1) ? (int)(tri_pick_r(s, m) * g.w + tri_pick_c(s, m)) : -1;
         }
     }
     for (int64_t p = p0; p < p1; ++p) {

@@ -31,7 +31,7 @@ __device__ __forceinline__ int bwd_taps(const Geom& g, int64_t a, int64_t b, int
         const int64_t jj[4] = {s.j_n, s.j_n + 1, s.j_n, s.j_n + 1};
         if (interp == HG_NEAREST) {                       // geometry_np.py:498-512
             if ((s.valid >> s.argmin) & 1) {
-                idx[0] = ii[s.argmin] * g.w + jj[s.argmin];
+                idx[0] = (s.i_n + (s.argmin >> 1)) * g.w + s.j_n + (s.argmin & 1);   // ii / jj below
                 wt[0] = 1.0;
                 n = 1;
             }
@@ -45,7 +45,7 @@ __device__ __forceinline__ int bwd_taps(const Geom& g, int64_t a, int64_t b, int
         const TriSample s = tri_sample(g, a, b);
         if (interp == HG_NEAREST) {                       // geometry_torch.py:335-347
             if ((s.vk >> s.argmin) & 1) {
-                idx[0] = s.r[s.argmin] * g.w + s.c[s.argmin];
+                idx[0] = tri_pick_r(s, s.argmin) * g.w + tri_pick_c(s, s.argmin);
                 wt[0] = 1.0;
                 n = 1;
             }

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(TF_THREADS) void k_homography(
     const int64_t hw = g.h * g.w;
     if constexpr (NEAREST) {
         const int m = s.argmin;
-        const int64_t off = ((s.vk >> m) & 1) ? s.r[m] * g.w + s.c[m] : -1;
+        const int64_t off = ((s.vk >> m) & 1) ? tri_pick_r(s, m) * g.w + tri_pick_c(s, m) : -1;
         for (int64_t p = p0; p < p1; ++p)
             dst[p * n + q] = off >= 0 ? src[p * hw + off] : (Tout)0;
     } else {

@@ -66,9 +66,6 @@ namespace hg {
 #ifndef TU_PDP_VLD
 #define TU_PDP_VLD 4        // with TU_VLD: planes of rows held in VGPRs ahead of the one blended
 #endif
-#ifndef TU_NKMUL
-#define TU_NKMUL 1          // 'nearest' 8-bit: output columns per lane x this (A/B: 2 -> 8-B stores)
-#endif
 #ifndef TU_CPP
 #define TU_CPP 24           // planes per unit when the grid has a wave per unit (round 5)
 #endif
@@ -113,6 +110,10 @@ template <> struct UInt<2> { using T = unsigned short; };
 template <> struct UInt<4> { using T = unsigned; };
 
 // One lane's K-sample store of `bytes` = K * sizeof(Tout) bytes from the packed words v.
+// 12/16-byte stores take the row offset in the VGPR offset and soffset 0: with an SGPR soffset
+// the compiler puts no wait state between the store and a VALU write of its data registers,
+// and the MI355X then stored the overwritten value (bf16 -> f32 rows, r05;
+// tools/scan_store_hazard.py finds the pattern in device assembly).
 template <int BYTES>
 __device__ __forceinline__ void tu_store(const unsigned (&v)[4], __amdgpu_buffer_rsrc_t rs, unsigned vo,
                                          unsigned so) {
@@ -122,7 +123,7 @@ __device__ __forceinline__ void tu_store(const unsigned (&v)[4], __amdgpu_buffer
     else if constexpr (BYTES == 2) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v[0], rs, vo, so, 0);
     else if constexpr (BYTES == 4) __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, vo, so, 0);
     else if constexpr (BYTES == 8) __builtin_amdgcn_raw_buffer_store_b64(u2v{v[0], v[1]}, rs, vo, so, 0);
-    else __builtin_amdgcn_raw_buffer_store_b128(u4v{v[0], v[1], v[2], v[3]}, rs, vo, so, 0);
+    else __builtin_amdgcn_raw_buffer_store_b128(u4v{v[0], v[1], v[2], v[3]}, rs, vo + so, 0, 0);
 }
 
 template <typename T> __device__ __forceinline__ float tu_f32(unsigned bits) {
@@ -193,10 +194,18 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
             yo[k] = (unsigned)a * orow;
 #pragma unroll
             for (int kk = 0; kk < K; ++kk) {
+                if constexpr ((TU_DIAG & 4) != 0) {   // (diag: one record per unit, timing only)
+                    if (k > 0 || kk > 0) {
+                        for (int v = 0; v < NV; ++v) off[k][kk][v] = off[0][0][v] + kk * E;
+                        if constexpr (!NEAR)
+                            for (int v = 0; v < 3; ++v) wt[k][kk][v] = wt[0][0][v];
+                        continue;
+                    }
+                }
                 // one sample's fp64 temporaries at a time (the scheduler would otherwise
                 // interleave the samples and spill)
                 __builtin_amdgcn_sched_barrier(0);
-                const TriSample s = tri_sample(D.g, a, cb + kk);
+                const TriSample s = tri_sample_fast(D.g, a, cb + kk);   // (tri_fast_ok: host)
                 if (k == 0 && kk == 0) rlo = __builtin_amdgcn_readfirstlane((int)s.i_n);
                 auto ix = [&](int v) -> unsigned {           // vertex v's LDS byte offset
                     return (s.vk >> v) & 1
@@ -204,7 +213,14 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
                                : (unsigned)TU_PCB;           // row 0's zero slot
                 };
                 if constexpr (NEAR) {
-                    off[k][kk][0] = ix(s.argmin);
+                    // selects, not s.r[s.argmin]: a run-time index into the sample's arrays put
+                    // them in scratch (128 B per lane for every nearest kernel)
+                    const int am = s.argmin;
+                    const int rr = (int)(am == 0 ? s.r[0] : am == 1 ? s.r[1] : s.r[2]);
+                    const int cc = (int)(am == 0 ? s.c[0] : am == 1 ? s.c[1] : s.c[2]);
+                    off[k][kk][0] = (s.vk >> am) & 1 ? (unsigned)((rr - rlo) * TU_ROWB + (cc - xb) * E)
+                                                     : (unsigned)TU_PCB;
+                    asm volatile("" : "+v"(off[k][kk][0]));   // one sample's temporaries at a time
                 } else {
                     off[k][kk][0] = ix(0);
                     off[k][kk][1] = ix(1);
@@ -255,7 +271,7 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
             const unsigned po = pi < np ? (unsigned)pi * planeb : (unsigned)np * planeb;
 #pragma unroll
             for (int q = 0; q < TU_NR_; ++q) {
-                const unsigned so = po + (unsigned)min(rlo + q, D.h - 1) * rowb;
+                const unsigned so = TU_DIAG >= 2 ? 0x80000000u : po + (unsigned)min(rlo + q, D.h - 1) * rowb;
                 rv[SL][q][0] = __builtin_amdgcn_raw_buffer_load_b32(xr, voff0, so, 0);
                 rv[SL][q][1] = __builtin_amdgcn_raw_buffer_load_b32(xr, voff1v, so, 0);
             }
@@ -300,7 +316,7 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
                     if constexpr (SB == 32) pk[kk] = bits;
                     else pk[(kk * SB) / 32] |= bits << ((kk * SB) % 32);
                 }
-                tu_store<OB>(pk, yr, vo, __builtin_amdgcn_readfirstlane(so + yo[k]));
+                tu_store<OB>(pk, yr, (TU_DIAG & 1) ? 0x80000000u : vo, __builtin_amdgcn_readfirstlane(so + yo[k]));
             }
         };
         if constexpr (TU_VLD) {
@@ -377,8 +393,9 @@ static int tu_launch(const void* src, void* dst, TriUpGeom& D, hipStream_t st) {
     const int64_t tiles = (int64_t)D.nwin * D.nband;
     int64_t nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, (RESIDENT + tiles / 2) / tiles));
     bool grid = false;
-    // ('linear' only: 'nearest' u8 ran 0.407 -> 0.789 ms with it, profiles/r05/triup_grid_ab.txt)
-    if (!NEAR && !env_is("HYGRID_TU_GRID", "0") && D.planes >= 2 * TU_CPP) {
+    // ('nearest' too since its records no longer use scratch: with the 128-B-per-lane stack
+    // object the grid ran u8 0.407 -> 0.789 ms, profiles/r05/triup_grid_ab.txt; r05 tu A/Bs)
+    if (!env_is("HYGRID_TU_GRID", "0") && D.planes >= 2 * TU_CPP) {
         nchunk = std::max<int64_t>(nchunk, D.planes / TU_CPP);
         grid = true;
     }
@@ -425,6 +442,7 @@ int triup_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t plan
     if ((h * w * E) * 4 >= ((int64_t)1 << 31) || (h1 * w1 * EO) * 4 >= ((int64_t)1 << 31))
         return HG_EUNSUP;
     const Geom g = make_tri(h, w, h1, w1, op == HG_OP_HEXRESIZE ? 0.5 : 0.75);
+    if (!tri_fast_ok(g)) return HG_EUNSUP;
     // upsampling only: output steps of at most one input sample in both directions
     if ((double)(h - 1) > (double)(h1 - 1) || (w1 > 1 && (double)(w - 1) > (double)(w1 - 1)))
         return HG_EUNSUP;
@@ -436,8 +454,9 @@ int triup_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t plan
     // K output columns per lane: the natural width (one dword of input samples per lane:
     // 8 / 4 / 2 for 1 / 2 / 4-byte inputs; stores of <= 16 B), or one column when that window
     // of 64 K columns does not keep its vertices in the WC input columns or K does not divide w1
-    const int wc = TU_PCB / E, kn = std::max(1, (E == 1 ? 8 : E == 2 ? 4 : 2) / (near_ ? 2 : 1) / TU_KDIV) *
-                                    (near_ && E == 1 ? TU_NKMUL : 1);
+    // ('nearest' used half that width while its records spilled to scratch; without the spill
+    // the full width is faster: u8 0.297 -> 0.254 ms, r05 tu A/Bs)
+    const int wc = TU_PCB / E, kn = std::max(1, (E == 1 ? 8 : E == 2 ? 4 : 2) / TU_KDIV);
     int K = 0;
     for (const int k : {kn, 1})
         if (!K && w1 % k == 0 && tsk_lattice_ok(g, 64 * k, wc, 4 / E, D.qmin, qmax)) K = k;
@@ -451,9 +470,9 @@ int triup_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t plan
 #define HG_TU_K(TI, TO, KN, NR_)                                                                \
     return K == 1 ? tu_launch<TI, TO, 1, NR_>(src, dst, D, st) : tu_launch<TI, TO, KN, NR_>(src, dst, D, st);
     if (near_) {
-        if (E == 1) { HG_TU_K(uint8_t, uint8_t, 4 * TU_NKMUL / TU_KDIV, true) }
-        if (E == 2) { HG_TU_K(unsigned short, unsigned short, (2 / TU_KDIV > 0 ? 2 / TU_KDIV : 1), true) }
-        HG_TU_K(unsigned, unsigned, 1, true)
+        if (E == 1) { HG_TU_K(uint8_t, uint8_t, 8 / TU_KDIV, true) }
+        if (E == 2) { HG_TU_K(unsigned short, unsigned short, 4 / TU_KDIV, true) }
+        HG_TU_K(unsigned, unsigned, (2 / TU_KDIV > 0 ? 2 / TU_KDIV : 1), true)
     }
 #define HG_TU_OUT(TI, KN)                                                                       \
     if (ddt == HG_BF16) { HG_TU_K(TI, __bf16, KN, false) }                                      \
