@@ -64,7 +64,8 @@ namespace hg {
 #define TU_VLD 1            // 1: input rows by dword loads into VGPRs, PDP planes ahead, written to a
 #endif                      // one-plane LDS slot when consumed (instead of LDS-DMA into a ring)
 #ifndef TU_PDP_VLD
-#define TU_PDP_VLD 4        // with TU_VLD: planes of rows held in VGPRs ahead of the one blended
+#define TU_PDP_VLD 3        // with TU_VLD: planes of rows held in VGPRs ahead of the one blended
+                            // (4 spilled 24-28 B per lane in the f16-input linear kernels)
 #endif
 #ifndef TU_CPP
 #define TU_CPP 24           // planes per unit when the grid has a wave per unit (round 5)
