@@ -3,9 +3,18 @@ of more than 8 bytes (buffer_store_dwordx3 / x4) whose soffset is an SGPR, follo
 (no wait state) by a VALU instruction that writes one of the store's data VGPRs.  LLVM's hazard
 recognizer inserts the wait state only when soffset is not a register; on the MI355X the
 store was observed to send the overwritten value (tests/test_gpu_triup.py, bf16 -> f32).
-usage: python tools/scan_store_hazard.py FILE.s ...   (hipcc -S --cuda-device-only output)"""
+usage: python tools/scan_store_hazard.py FILE.s ...   (hipcc -S --cuda-device-only output)
+       python tools/scan_store_hazard.py --lib LIB.so   (every gfx950 code object in the library's
+                                                          .hip_fatbin, via clang-offload-bundler and
+                                                          llvm-objdump)"""
+import concurrent.futures
+import os
 import re
+import subprocess
 import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
 
 STORE = re.compile(r"^\s*buffer_store_dwordx([34])\s+v\[(\d+):(\d+)\],\s*\S+,\s*s\[\d+:\d+\],\s*(\S+)")
 VALU = re.compile(r"^\s*(v_\S+)\s+v\[?(\d+)(?::(\d+))?\]?")
@@ -18,6 +27,8 @@ def scan(path):
     for i, ln in enumerate(lines):
         if re.match(r"^_Z\S+:", ln):
             fn = ln.split(":")[0]
+        elif re.match(r"^[0-9a-f]+ <_Z\S+>:", ln):          # llvm-objdump label
+            fn = ln.split("<")[1].split(">")[0]
         m = STORE.match(ln)
         if not m or not m.group(4).startswith("s"):
             continue
@@ -36,9 +47,40 @@ def scan(path):
     return hits
 
 
+def disassemble_lib(lib, out_dir):
+    """The library's device code objects as llvm-objdump listings in out_dir (one per bundle)."""
+    fat = os.path.join(out_dir, "fatbin.bin")
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, fat], check=True)
+    data = open(fat, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    offs, i = [], data.find(magic)
+    while i >= 0:
+        offs.append(i)
+        i = data.find(magic, i + 1)
+
+    def one(k):
+        b = os.path.join(out_dir, f"b{k}.bin")
+        co = os.path.join(out_dir, f"co{k}.o")
+        open(b, "wb").write(data[offs[k]:offs[k + 1] if k + 1 < len(offs) else len(data)])
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={b}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        s_path = os.path.join(out_dir, f"co{k}.s")
+        with open(s_path, "w") as f:
+            subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], stdout=f, check=True)
+        return s_path
+
+    with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        return list(ex.map(one, range(len(offs))))
+
+
 if __name__ == "__main__":
     total = 0
-    for p in sys.argv[1:]:
+    paths = sys.argv[1:]
+    tmp = None
+    if paths[:1] == ["--lib"]:
+        tmp = tempfile.TemporaryDirectory()
+        paths = disassemble_lib(paths[1], tmp.name)
+    for p in paths:
         for fn, ln, st, nx in scan(p):
             total += 1
             print(f"{p}:{ln}: {fn}\n    {st}\n    {nx}")
