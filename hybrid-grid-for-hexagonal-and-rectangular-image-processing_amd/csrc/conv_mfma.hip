@@ -398,6 +398,9 @@ __device__ __forceinline__ void cd_wait_vm() {
 // MFMAs cover each other's waits)
 // NQT: 16-column tiles per workgroup (4; 3 with PSB1 = one raw-P buffer is the 4-waves-per-SIMD
 // build: 48 accumulators and <= 40 KB of LDS, so four workgroups fit a CU; round 5)
+#ifndef CD_OPQ
+#define CD_OPQ 1                      // DMA address terms recomputed per chunk (see dma_w)
+#endif
 #ifndef CD_WPE3
 #define CD_WPE3 4                     // waves per SIMD asked of the allocator for the NQT 3 build
 #endif
@@ -468,12 +471,19 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)wf, (short)0, 0x7fffffff, 0x00020000);
 
+    // CD_OPQ: the DMA address terms are recomputed at every chunk from values the compiler
+    // cannot see through (no hoisting: the hoisted per-piece offsets spilled 57-73 SGPRs)
+    auto opq = [](int v) {
+        if constexpr (CD_OPQ) asm volatile("" : "+s"(v));
+        return v;
+    };
     auto dma_w = [&](int ci) {                            // chunk ci's weights -> buffer
         const int buf = WDB ? (ci & 1) : 0;
+        const int wvo = opq(wv);
         // weights: pieces j = wv * WPW + i of the chunk's (pt, kb) blocks of CM_O * 4 fragments
 #pragma unroll
         for (int i = 0; i < WPW; ++i) {
-            const int j = wv * WPW + i;
+            const int j = wvo * WPW + i;
             const int blk = j / (CM_O / 16), part = j % (CM_O / 16);   // (pt * 2 + kb), 1-KiB part
             const unsigned so = (unsigned)((((int64_t)ci * 6 + blk) * Opad + o0) * 64 + part * 1024);
             const unsigned lda = lds0 + LPSB + buf * LWSB + (blk * CM_O * 4) * 16 + part * 1024;
@@ -487,13 +497,14 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
     auto dma_p = [&](int ci) {                            // chunk ci's raw P rows -> buffer (ci & 1)
         const int buf = PSB1 ? 0 : ci & 1;
         if (interior) {
+            const int wvo = opq(wv), ho = opq(G.h), wo = opq(G.w);
             // P rows: pieces j = wv * PPW + i = (cc, pr); lanes 0-39 one dword each
 #pragma unroll
             for (int i = 0; i < PPW; ++i) {
-                const int j = wv * PPW + i;
+                const int j = wvo * PPW + i;
                 const int cc = j / CM_PR, pr = j % CM_PR;
                 const int c = ci * CM_CC + cc;
-                const unsigned so = c < G.C ? (unsigned)((((int64_t)c * G.h + (r0 + pr - G.p)) * G.w + xs) * 2)
+                const unsigned so = c < G.C ? (unsigned)((((int64_t)c * ho + (r0 + pr - G.p)) * wo + xs) * 2)
                                             : 0x80000000u;
                 const unsigned lda = lds0 + LPSB + NWB * LWSB + buf * LPRAW + j * CD_PRW * 4;
                 const unsigned vo = lane * 4u;

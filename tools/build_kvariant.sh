@@ -12,7 +12,9 @@ OBJ=$PKG/build/obj
 OUT=$PKG/HyGrid/_lib/variants
 mkdir -p "$OUT" "$OBJ/variants"
 base=$(basename "$SRC" .hip)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize "$@" \
+# SLP=1: keep the SLP vectoriser (the Makefile's default for most objects)
+slp=-fno-slp-vectorize; [ "${SLP:-0}" = 1 ] && slp=
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $slp "$@" \
     -I"$PKG/csrc" -c "$PKG/csrc/$SRC" -o "$OBJ/variants/${base}_$NAME.o"
 objs=()
 # FULL=1: every object of the library (for entry points outside the fused pipeline, e.g. the conv)
