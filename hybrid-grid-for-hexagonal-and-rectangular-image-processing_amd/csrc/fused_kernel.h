@@ -931,9 +931,13 @@ void k_fused(const Tin* __restrict__ x,
             const int c0 = j_n - (i_n + 1) / 2, c1 = j_n - (i_n + 2) / 2;
             const int d0 = c0 - 2 * bo, d1 = c1 - 2 * bo;
             const bool r1in = i_n + 1 < F.h1;
-            const bool v1 = c0 >= 0 && c0 < F.w1;
-            const bool v2 = flag ? (r1in && c1 >= 0 && c1 < F.w1) : (c0 + 1 >= 0 && c0 + 1 < F.w1);
-            const bool v3 = r1in && c1 + 1 >= 0 && c1 + 1 < F.w1;
+            // vertex validity (bitwise, no short-circuit branches; only the clamped-column
+            // paths below need it)
+            auto vflags = [&](bool& v1, bool& v2, bool& v3) {
+                v1 = (c0 >= 0) & (c0 < F.w1);
+                v2 = flag ? (r1in & (c1 >= 0) & (c1 < F.w1)) : ((c0 + 1 >= 0) & (c0 + 1 < F.w1));
+                v3 = r1in & (c1 + 1 >= 0) & (c1 + 1 < F.w1);
+            };
             const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a * yrow));
             if constexpr (PLDS) {
                 // conv row 2a + 1 next to row 2a (written at the previous step); per-lane
@@ -954,6 +958,8 @@ void k_fused(const Tin* __restrict__ x,
                     a2 = flag ? (r1in ? O * ZW + c1 - W0 : 128) : r0b + c0 + 1 - W0;
                     a3 = r1in ? O * ZW + c1 + 1 - W0 : 128;
                 } else {
+                    bool v1, v2, v3;
+                    vflags(v1, v2, v3);
                     auto col = [&](int c) { return min(max(c - W0, 0), 127); };
                     a1 = v1 ? r0b + col(c0) : 128;
                     a2 = v2 ? (flag ? O * ZW + col(c1) : r0b + col(c0 + 1)) : 128;
@@ -972,6 +978,8 @@ void k_fused(const Tin* __restrict__ x,
                 }
                 return;
             }
+            bool v1, v2, v3;
+            vflags(v1, v2, v3);
     #pragma unroll
             for (int o = 0; o < O; ++o) {
                 const fu_f2 z0 = e1 ? Z1[o] : ZK[o], z1 = Z1[o];
