@@ -47,8 +47,8 @@ def scan(path):
     return hits
 
 
-def disassemble_lib(lib, out_dir):
-    """The library's device code objects as llvm-objdump listings in out_dir (one per bundle)."""
+def split_bundles(lib, out_dir):
+    """The library's gfx950 code objects (one per offload bundle of .hip_fatbin) in out_dir."""
     fat = os.path.join(out_dir, "fatbin.bin")
     subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, fat], check=True)
     data = open(fat, "rb").read()
@@ -57,20 +57,29 @@ def disassemble_lib(lib, out_dir):
     while i >= 0:
         offs.append(i)
         i = data.find(magic, i + 1)
-
-    def one(k):
+    cos = []
+    for k, o in enumerate(offs):
         b = os.path.join(out_dir, f"b{k}.bin")
         co = os.path.join(out_dir, f"co{k}.o")
-        open(b, "wb").write(data[offs[k]:offs[k + 1] if k + 1 < len(offs) else len(data)])
+        open(b, "wb").write(data[o:offs[k + 1] if k + 1 < len(offs) else len(data)])
         subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={b}",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
-        s_path = os.path.join(out_dir, f"co{k}.s")
+        cos.append(co)
+    return cos
+
+
+def disassemble_lib(lib, out_dir):
+    """The library's device code objects as llvm-objdump listings in out_dir (one per bundle)."""
+    cos = split_bundles(lib, out_dir)
+
+    def one(co):
+        s_path = co[:-2] + ".s"
         with open(s_path, "w") as f:
             subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], stdout=f, check=True)
         return s_path
 
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
-        return list(ex.map(one, range(len(offs))))
+        return list(ex.map(one, cos))
 
 
 if __name__ == "__main__":
