@@ -8,14 +8,20 @@ radius 2, padding=1, bias; weights drawn with torch.manual_seed(3) and the
 reference initialiser) -> hex->rect linear resample (2160x3840), all on the
 gfx950 kernels of libhygrid_hip.so, with bf16 tensors between stages.
 
-Multi-GPU: one process per GPU (torchrun); every rank owns its own 128 images
-(weak scaling, no data-path collective).  value = all ranks' input pixels / the
-max-over-ranks wall time of K steps.  Every timed step ends with per-image,
-per-channel sums of a row sample of its output (every 64th row), all-gathered over
-RCCL at N > 1 (the collective stays inside the timed loop; a few KB per
-rank).  After the timed region, full per-image checksums are all-gathered, and
-(N>1) the full-output gather to rank 0 is timed and reported on its own
-(`gather`), never folded into `value`.
+Multi-GPU: one process per GPU; every rank owns its own 128 images (weak scaling, no
+data-path collective).  `--gpus N` with N > 1 and no WORLD_SIZE in the environment starts
+`torch.distributed.run --nproc-per-node N` as a CHILD process (nothing here has touched the
+GPU yet; never an exec) and exits with its return code; under a launcher, WORLD_SIZE must
+equal --gpus or the bench exits with status 2.  value = all ranks' input pixels / the
+max-over-ranks wall time of K steps.  Every timed step, at every N including N = 1 (a
+world-1 process group), ends with per-image, per-channel sums of a row sample of its output
+(every 64th row) all-gathered over RCCL (the collective stays inside the timed
+loop; a few KB per rank), so the per-step work is the same at every N.  After the timed
+region, full per-image checksums are all-gathered, and (N>1) the full-output gather to
+rank 0 is timed and reported on its own (`gather`), never folded into `value`.
+`--dry-run`: the same launch, process groups (gloo), barriers, per-step collective,
+max-over-ranks timing and JSON line on the CPU with a stand-in step and no HIP kernel
+(tests/test_bench_launch.py); its value is not a measurement.
 
 Extra JSON fields: `kernels` (per-stage HIP-event times and algorithmic GB/s),
 `roofline` (dominant kernel vs 8 TB/s HBM), `cpu_baseline` (the C/OpenMP oracle
@@ -37,11 +43,14 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# What bounds the headline kernel, from the shipped build's code object (124 VGPRs, 102 SGPRs,
-# no spills: 4 waves per SIMD) and its SQ counters (profiles/r05/).
-FUSED4_LIMITER = ("VALU issue and memory together for the fused kernel (k_fused4: 4 columns per "
-                  "lane, 124 VGPRs, 4 waves per SIMD; 126 packed stencil FMAs + r2h / h2r per "
-                  "240-column wave-step, ~88 % of SIMD cycles issuing VALU)")
+# What bounds the headline kernel (DESIGN.md section 6, round 5 measurements): its
+# cache-resident build (every load / store hits one row) runs 1.83-2.02 ms, the real one
+# ~0.7 ms more; loads alone or stores alone add ~0.25 ms each, both together ~0.7 ms.
+FUSED4_LIMITER = ("memory latency on top of VALU issue (k_fused4: 124 VGPRs, 4 waves per SIMD, "
+                  "1 rect row of prefetch): cache-resident floor 1.83-2.02 ms per 4K b128 launch, "
+                  "the interleaved row-load / row-store stream adds ~0.7 ms that does not "
+                  "overlap with the stencil (profiles/r05/fused4_floor_ab.txt, "
+                  "fused4_additivity_ab.txt)")
 PEAK_BPS = HBM_PEAK_GBS * 1e9
 
 
@@ -86,6 +95,9 @@ def parse():
                     help="N > 1 with every rank on cuda:0 and the collectives over gloo (host "
                          "staged): exercises the multi-rank bench path on a one-GPU box; the "
                          "ranks share one GPU, so the value is not a scaling measurement")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: the launcher, process groups (gloo), barriers, per-step "
+                         "collective, timing and JSON line with a CPU stand-in step (tests)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-kernel HBM bytes from rocprofv3 PMC passes (optional)")
     return ap.parse_args()
@@ -249,74 +261,143 @@ def bench_lattices(ops, measure, gen, dev, world, Bl, C, H, W):
     return out
 
 
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` (N > 1) outside a launcher: run this script under torch.distributed.run as a
+    child process, one rank per GPU on 127.0.0.1, and return its exit status.  Called before
+    anything here touches the GPU; the parent only waits (no exec)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on these hosts
+    log("bench: launching", n, "ranks:", " ".join(cmd))
+    return subprocess.run(cmd, env=env).returncode
+
+
+class CpuEvent:
+    """torch.cuda.Event's record / elapsed_time on the host clock (--dry-run)."""
+    def __init__(self, **_):
+        self.t = None
+
+    def record(self):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, end):
+        return (end.t - self.t) * 1e3
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        log("bench: --gpus must be >= 1")
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: the line would report the wrong "
+            f"n_gpus; launch with --nproc-per-node {args.gpus} or drop the launcher")
+        sys.exit(2)
+    dry = args.dry_run
     rehearse = world > 1 and args.rehearse_gloo
-    if rehearse:
+    # every N has a process group (N = 1: world 1 on an in-process store), so the per-step
+    # collective runs at N = 1 too and the 1 -> N efficiency compares equal per-step work
+    pg_kw = {} if world > 1 else {"store": dist.HashStore(), "rank": 0, "world_size": 1}
+    if dry or rehearse:
         local_rank = 0
-        dist.init_process_group("gloo")
-    elif world > 1:
+        dist.init_process_group("gloo", **pg_kw)
+    else:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
-    cdev = torch.device("cpu") if rehearse else dev   # where the collectives' tensors live
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), **pg_kw)
+    dev = torch.device("cpu") if dry else torch.device("cuda", local_rank)
+    if not dry:
+        torch.cuda.set_device(dev)
+    cdev = torch.device("cpu") if (rehearse or dry) else dev   # where the collectives' tensors live
+    Event = CpuEvent if dry else torch.cuda.Event
 
-    from HyGrid import ops
-    from HyGrid.HexFrames import HexConv2d
-    from HyGrid.pipeline import rect_hex_conv_rect, rect_hex_rect
+    def sync():
+        if not dry:
+            torch.cuda.synchronize()
 
     B, C, H, W = args.batch, args.channels, args.height, args.width
     bf16 = torch.bfloat16
-    gen = torch.Generator(device=dev).manual_seed(2 + rank)
-    x = torch.rand((B, C, H, W), generator=gen, device=dev, dtype=bf16)
-    torch.manual_seed(3)
-    conv = HexConv2d(C, C, 0, 2, padding=1, groups=1, bias=True).to(dev)
-    conv.out_dtype = bf16
+    if dry:
+        # stand-in step on the host: no HIP kernel runs, the value is not a measurement
+        B, H, W = min(B, 4), min(H, 64), min(W, 128)
+        gen = torch.Generator().manual_seed(2 + rank)
+        x = torch.rand((B, C, H, W), generator=gen, dtype=torch.float32)
+        conv = None
 
-    def run_unfused(record, ev):
-        if record:
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            e[0].record()
-        h = ops.rect_to_hex(x, (H, W), out_dtype=bf16)
-        if record:
-            e[1].record()
-        c = conv(h)
-        if record:
-            e[2].record()
-        y = ops.hex_to_rect(c, (H, W), out_dtype=bf16)
-        if record:
-            e[3].record()
-            ev.append(e)
-        return y
+        def run_fused(record, ev):
+            if record:
+                e = [Event(enable_timing=True) for _ in range(2)]
+                e[0].record()
+            y = (x * 0.75 + 0.125).to(bf16)
+            if record:
+                e[1].record()
+                ev.append(e)
+            return y
+        run_unfused = run_fused
+    else:
+        from HyGrid import ops
+        from HyGrid.HexFrames import HexConv2d
+        from HyGrid.pipeline import rect_hex_conv_rect, rect_hex_rect
 
-    def run_fused(record, ev):
-        if record:
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            e[0].record()
-        y = rect_hex_conv_rect(x, conv, (H, W), (H, W), out_dtype=bf16)
-        if record:
-            e[1].record()
-            ev.append(e)
-        return y
+        gen = torch.Generator(device=dev).manual_seed(2 + rank)
+        x = torch.rand((B, C, H, W), generator=gen, device=dev, dtype=bf16)
+        torch.manual_seed(3)
+        conv = HexConv2d(C, C, 0, 2, padding=1, groups=1, bias=True).to(dev)
+        conv.out_dtype = bf16
+
+        def run_unfused(record, ev):
+            if record:
+                e = [Event(enable_timing=True) for _ in range(4)]
+                e[0].record()
+            h = ops.rect_to_hex(x, (H, W), out_dtype=bf16)
+            if record:
+                e[1].record()
+            c = conv(h)
+            if record:
+                e[2].record()
+            y = ops.hex_to_rect(c, (H, W), out_dtype=bf16)
+            if record:
+                e[3].record()
+                ev.append(e)
+            return y
+
+        def run_fused(record, ev):
+            if record:
+                e = [Event(enable_timing=True) for _ in range(2)]
+                e[0].record()
+            y = rect_hex_conv_rect(x, conv, (H, W), (H, W), out_dtype=bf16)
+            if record:
+                e[1].record()
+                ev.append(e)
+            return y
 
     from HyGrid.dist import gather_sums
     sums_buf = {}
 
     def step_sums(y):
-        """Per-image, per-channel sums of every 64th output row, all-gathered over RCCL at
-        N > 1: the collective every timed step ends with (a few KB per rank).  One strided
-        reduction kernel accumulating in fp32; nothing at N = 1 (no collective to feed)."""
-        if world > 1:
-            s_ = torch.sum(y[:, :, ::64], (2, 3), dtype=torch.float32).to(cdev)
-            key = tuple(s_.shape)
-            if key not in sums_buf:
-                sums_buf[key] = torch.empty((world * s_.shape[0],) + key[1:], dtype=s_.dtype,
-                                            device=cdev)
-            gather_sums(s_, out=sums_buf[key])
+        """Per-image, per-channel sums of every 64th output row, all-gathered over RCCL: the
+        collective every timed step ends with (a few KB per rank), at every N (N = 1: the
+        world-1 group).  One strided reduction kernel accumulating in fp32."""
+        s_ = torch.sum(y[:, :, ::64], (2, 3), dtype=torch.float32).to(cdev)
+        key = tuple(s_.shape)
+        if key not in sums_buf:
+            sums_buf[key] = torch.empty((world * s_.shape[0],) + key[1:], dtype=s_.dtype,
+                                        device=cdev)
+        gather_sums(s_, out=sums_buf[key])
 
     def measure(fn, steps, warmup, collective=True):
         """W untimed steps, then K steps between barrier + synchronize; max over ranks."""
@@ -326,22 +407,19 @@ def main():
                 y = fn(False, ev)
                 if collective:
                     step_sums(y)
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
-            torch.cuda.synchronize()
+            sync()
+            dist.barrier()
+            sync()
             t0 = time.perf_counter()
             for _ in range(steps):
                 y = fn(True, ev)
                 if collective:
                     step_sums(y)
-            torch.cuda.synchronize()
-            if world > 1:
-                dist.barrier()
+            sync()
+            dist.barrier()
             t1 = time.perf_counter()
         el = torch.tensor([t1 - t0], dtype=torch.float64, device=cdev)
-        if world > 1:
-            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
         n = len(ev[0]) - 1
         # per-kernel times from HIP events recorded on the launch stream
         stage_ms = [sum(e[i].elapsed_time(e[i + 1]) for e in ev) / len(ev) for i in range(n)]
@@ -359,9 +437,8 @@ def main():
             while time.perf_counter() < t_end:
                 for _ in range(8):
                     step_sums(fn(False, ev_))
-                torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+                sync()
+        dist.barrier()
 
     def measure_line(fn, steps):
         """A secondary line: 100 ms of untimed pre-warm of its own step and max(3, W) warmup
@@ -372,7 +449,7 @@ def main():
             t_end = time.perf_counter() + 0.1
             while time.perf_counter() < t_end:
                 fn(False, [])
-                torch.cuda.synchronize()
+                sync()
         return measure(fn, steps, max(3, args.warmup), collective=False)
 
     img_bytes = B * C * H * W * 2          # one bf16 batch tensor
@@ -393,7 +470,7 @@ def main():
     dom = max(stages, key=lambda s: stage_ms[s])
     achieved = alg_bytes[dom] / (stage_ms[dom] * 1e-3) / 1e9
     traffic, traffic_note = None, "no PMC profile"
-    if os.path.exists(args.pmc_json):
+    if not dry and os.path.exists(args.pmc_json):
         try:
             from HyGrid._abi import kernel_source_digest
             with open(args.pmc_json) as f:
@@ -418,7 +495,7 @@ def main():
                 if dom == "pipeline_r2h_conv_h2r" else "hbm"}
 
     compare = None
-    if not args.unfused and not args.no_compare:
+    if not args.unfused and not dry and not args.no_compare:
         # the three-operator chain on the same data, reported beside `value` (never as it)
         steps_u = max(2, args.steps // 2)
         _, el_u, sms_u = measure_line(run_unfused, steps_u)
@@ -431,7 +508,7 @@ def main():
                                for k, m in zip(ks, sms_u)}}
 
     pyramid = None
-    if not args.unfused and not args.no_pyramid:
+    if not args.unfused and not dry and not args.no_pyramid:
         # BASELINE configs[4], per GPU: 8K fp16 rasters, r2h at full
         # size, then 3 x [depthwise HexConv2d(3,3,0,2,padding=1,groups=3) with Gaussian
         # taps [1,1,1,6,1,1,1]/12 -> hexresize to (h//2, w//2)].  Reported beside
@@ -534,7 +611,7 @@ def main():
         del xp
 
     roundtrip = None
-    if not args.unfused and not args.no_roundtrip:
+    if not args.unfused and not dry and not args.no_roundtrip:
         # BASELINE configs[1]: 1080p RGB fp32, batch 32 per GPU,
         # rect->hex bilinear -> hex->rect linear.  Reported beside `value`, never as it.
         Hr, Wr, Br = 1080, 1920, 32
@@ -589,7 +666,7 @@ def main():
         del xr
 
     wide = None
-    if not args.unfused and not args.no_wide_conv:
+    if not args.unfused and not dry and not args.no_wide_conv:
         # HexConvModule-sized HexConv2d (HexModules.py:97-288): 64 -> 64 channels on a
         # 1080p bf16 batch of 4, the implicit GEMM on the bf16 matrix cores with every fp32
         # weight split into three bf16 parts (conv_mfma.hip, k_hexconv_mfma_bf16: exact
@@ -629,7 +706,7 @@ def main():
         del xw
 
     lattices = None
-    if not args.unfused and not args.no_lattices:
+    if not args.unfused and not dry and not args.no_lattices:
         lattices = bench_lattices(ops, measure_line, gen, dev, world, args.lattice_batch, C, H, W)
 
     # checksums over RCCL (not timed), and the full-output gather on its own
@@ -638,7 +715,7 @@ def main():
     gather = None
     if world > 1:
         cs = gather_checksums(cs.to(cdev))
-        if not args.no_gather and not rehearse:
+        if not args.no_gather and not rehearse and not dry:
             try:
                 gather_to_root(y)            # warm the RCCL channels
                 torch.cuda.synchronize()
@@ -657,7 +734,7 @@ def main():
     checksum = float(cs[..., 0].sum().item())
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_images > 0:
+    if rank == 0 and world == 1 and args.cpu_images > 0 and not dry:
         try:
             cpu = cpu_baseline(args, conv.kernel.detach().cpu().numpy(),
                                conv.bias.detach().cpu().numpy())
@@ -683,11 +760,17 @@ def main():
             "unfused": compare, "roundtrip": roundtrip, "pyramid": pyramid, "wide_conv": wide,
             "lattices": lattices,
             "gather": gather, "checksum": checksum,
-            "device": torch.cuda.get_device_name(dev),
+            "device": "cpu (dry run)" if dry else torch.cuda.get_device_name(dev),
         }
+        if dry:
+            line["dry_run"] = True
+            line["data"] = ("--dry-run: a host stand-in step (no HIP kernel) on a "
+                            f"{B}x{C}x{H}x{W} tensor; launcher / collectives / timing only, the "
+                            "value is not a measurement")
+        if line["n_gpus"] != args.gpus:
+            raise SystemExit(f"bench: n_gpus {line['n_gpus']} != --gpus {args.gpus}")
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -13,6 +13,7 @@
 #   "pmc KERNEL CMD..."     FETCH/WRITE + SQ passes over one kernel (tools/pmc_kernel.sh)
 #   "final"                 end-of-round evidence (tools/final_session.sh) + fused SQ passes
 #   "mb NAME ARGS..."       run a microbenchmark binary tools/microbench/NAME (built on the host)
+#   "mbpmc NAME ALG ARGS"   the same, then its kernel trace + FETCH/WRITE passes (tools/mb_pmc.sh)
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
@@ -47,6 +48,7 @@ for S in "$@"; do
                bash tools/pmc_fused.sh "$TAG/final/sq" fused 32 >> "$log" 2>&1; rc=$?; tail -30 "$log" ;;
     mb)    b=$1; shift
            timeout -k 10 300 tools/microbench/$b "$@" >> "$log" 2>&1; rc=$?; tail -30 "$log" ;;
+    mbpmc) bash tools/mb_pmc.sh "$TAG/mbpmc_$n" "$@" >> "$log" 2>&1; rc=$?; tail -40 "$log" ;;
     *)     echo "unknown step kind: $kind"; rc=2 ;;
     esac
     if [ $rc -ne 0 ]; then echo "step $n failed (rc $rc): $S"; exit $rc; fi
