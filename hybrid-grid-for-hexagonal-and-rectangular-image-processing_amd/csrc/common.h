@@ -64,6 +64,18 @@ inline bool env_is(const char* name, const char* value) {
 // share 128-B lines, are fetched into the same L2 instead of into two
 // (cdna_hip_programming.md T1, bijective form for nwg % 8 != 0).  Speed only: any
 // placement is correct.
+// Every buffer store wider than 8 bytes goes through this: the row offset is added into the
+// VGPR offset and soffset is 0.  With an SGPR soffset the compiler's hazard recognizer puts no
+// wait state between a > 8-byte MUBUF store and a VALU write of its data registers, and the
+// MI355X then stored the overwritten value (k_tri_up, round 5; tests/test_store_hazard.py scans
+// the built library for the pattern).  A voff of 0x80000000 (a dropped store) stays out of
+// range: every soff here is a byte offset inside a buffer of < 2^31 bytes.
+typedef unsigned hg_u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void hg_store_b128(hg_u4v v, __amdgpu_buffer_rsrc_t rs, unsigned voff,
+                                              unsigned soff) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff + soff, 0, 0);
+}
+
 __device__ __forceinline__ unsigned xcd_swizzle(unsigned bid, unsigned nwg) {
     const unsigned q = nwg >> 3, r = nwg & 7u, x = bid & 7u;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);

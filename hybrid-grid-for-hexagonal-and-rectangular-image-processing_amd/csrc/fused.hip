@@ -82,9 +82,6 @@ static bool fused_geometry_ok(const Geom& g) {
     return true;
 }
 
-// rt4.hip: the 4-column round trip (16-bit / fp32 in and out, widths a multiple of 4), or HG_EUNSUP
-int rt4_try(const void* x, void* y, int x_dtype, int y_dtype, const FusedGeom& F0, hipStream_t st);
-
 // Round trip rect -> hex -> rect without the conv (MD 2), one plane per "image" (C = 1):
 // geometry_np.hex_to_rect_resample(rect_to_hex_resample(x, (h1, w1)), (h1, w1)) with the hex
 // image kept on chip in fp32.
@@ -104,10 +101,6 @@ int fused_rt_try(const void* x, void* y, int x_dtype, int y_dtype, int64_t plane
     F.rys = g.ys;
     F.nwin = (int)((w1 + FU_OWN - 1) / FU_OWN);
     F.nband = (int)((h1 + fu_rb(2) - 1) / fu_rb(2));
-    {
-        const int rc4 = rt4_try(x, y, x_dtype, y_dtype, F, st);   // rt4.hip: 4 columns per lane
-        if (rc4 != HG_EUNSUP) return rc4;
-    }
     const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + FU_GW - 1) / FU_GW);
     if (blocks > INT_MAX) return HG_ESHAPE;
     const dim3 grid((unsigned)blocks), blk(FU_THREADS);
@@ -188,25 +181,15 @@ int fused_try(const void* x, const float* kernel, const float* bias, void* y, in
 
 namespace hg {
 void fused4_layout(int* band_rows, int* win_own, int* win_halo);
-void rt4_layout(int* band_rows, int* win_own, int* win_halo);
-void fconv4_layout(int* band_rows, int* win_own, int* win_halo);
 }
 
 // md 0-2: the two-column kernel's modes; md 6: MD 0's four-column variant (fused4.hip: bf16,
-// C = O = 3, widths a multiple of 4); md 7: MD 2's four-column variant (rt4.hip); md 8: MD 1's four-column
-// variant (fused4.hip: bf16, C = O = 3)
+// C = O = 3, widths a multiple of 4).  (md 7 / 8, round 5's four-column round trip and conv,
+// were removed in round 6: HG_EINVAL.)
 extern "C" int hg_fused_layout(int md, int* band_rows, int* win_own, int* win_halo) {
     if (!band_rows || !win_own || !win_halo) return HG_EINVAL;
     if (md == 6) {
         hg::fused4_layout(band_rows, win_own, win_halo);
-        return HG_OK;
-    }
-    if (md == 7) {
-        hg::rt4_layout(band_rows, win_own, win_halo);
-        return HG_OK;
-    }
-    if (md == 8) {
-        hg::fconv4_layout(band_rows, win_own, win_halo);
         return HG_OK;
     }
     if (md < 0 || md > 2) return HG_EINVAL;

@@ -15,7 +15,9 @@
 // in in-process A/Bs on three boxes, profiles/r04/f4/).
 //
 // Domain: fused_try's (same-size lattice, padding 1, value 0) with bf16 in and out, C = O = 3,
-// groups 1, w and w2 multiples of 4.  Results within the fp32 rounding of k_fused MD 0 (the same
+// groups 1, w and w2 multiples of 4.  (Round 5 also built this layout for HexConv2d alone and
+// for the round trip, and a per-wave LDS-DMA row ring and cache-policy variants of this kernel:
+// all measured slower; removed in round 6.)  Results within the fp32 rounding of k_fused MD 0 (the same
 // products and sums per output; a tap order may differ), checked against the oracle chain.
 #include <climits>
 #include <cmath>
@@ -40,25 +42,8 @@ namespace hg {
 #ifndef F4_WPE
 #define F4_WPE 4                       // waves per SIMD asked of the register allocator
 #endif
-#ifndef F4_DMA
-#define F4_DMA 0                       // rect rows by per-wave LDS-DMA into a 6-row LDS ring (2-3
-                                       // steps ahead, no VGPRs, no workgroup barrier) instead of
-                                       // the register ring
-#endif
-#ifndef F4_SAUX
-#define F4_SAUX 0                      // cache-policy bits of the output stores (A/B: 2 nt, 16 sc1)
-#endif
-#ifndef F4_LAUX
-#define F4_LAUX 0                      // ... of the rect-row loads
-#endif
-#ifndef F4_DIAG_NOBEL
-#define F4_DIAG_NOBEL 0                // diagnostic (wrong results): skip the stencil's 'below' taps
-                                       // (36 of 132 packed FMAs per step) to test whether compute and
-                                       // memory time add or overlap
-#endif
-#ifndef F4_DIAG_NOFP64
-#define F4_DIAG_NOFP64 0               // diagnostic (wrong results): row table and column weights
-                                       // from constants instead of the fp64 lattice (prologue cost)
+#ifndef F4_REV
+#define F4_REV 1                       // odd full bands walk upwards (shared halo rows in L2, below)
 #endif
 #ifndef F4_NOMEM
 #define F4_NOMEM 0                     // diagnostic floor: every row load / store hits row 0 of its
@@ -68,11 +53,6 @@ namespace hg {
 constexpr int F4_GW = 4, F4_THREADS = 256;
 constexpr int F4_HL = 8, F4_OWN = 240;  // window halo (left) and owned columns
 constexpr int F4_RB = F4_RB_;
-#ifndef F4_RB_CONV_
-#define F4_RB_CONV_ 18                 // MD 1: output rows per band (k_fused MD 1's fastest)
-#endif
-constexpr int F4_RB_CONV = F4_RB_CONV_;
-static_assert(F4_RB_CONV % 6 == 0 && F4_RB_CONV > 0, "bands are whole 6-step blocks");
 static_assert(F4_RB % 6 == 0 && F4_RB > 0, "bands are whole 6-step blocks");
 
 typedef unsigned f4_u2 __attribute__((ext_vector_type(2)));
@@ -82,59 +62,51 @@ __device__ __forceinline__ void f4_unpack(f4_u2 r, fu_f2& a, fu_f2& b, unsigned 
     b = fu_f2{__builtin_bit_cast(float, r.y << 16), __builtin_bit_cast(float, r.y & hi16)};
 }
 
-// MD 0: rect -> hex -> HexConv2d -> hex -> rect (the headline).  MD 1: HexConv2d alone
-// (HexFrames.py:96-169, radius 2, stride 1, padding 1, pad value 0), as k_fused MD 1: the u rows
-// are the input rows (zeros outside the raster), no r2h / h2r, the conv rows stored as they
-// complete; the band length is F4_RB_CONV.
-template <int OP, int MD>
+// rect -> hex -> HexConv2d -> hex -> rect (the headline); OP = the stencil's tap column class
+// at padding 1 ((even_odd_offset + 1) & 1).
+//
+// Band direction (F4_REV, round 6): a band reads its 30 output rows' rect rows plus 2 halo rows
+// on each side, and the halo rows of two neighbouring bands are the same 4 rows.  Walking every
+// band downwards, band k + 1 reads them first (at its start) and band k last (at its end), a
+// whole band walk later, when they have long left the L2: the vertical halo comes from HBM
+// twice (34 / 30 = 1.133x the input bytes).  With F4_REV the odd full bands walk upwards, so the
+// two bands of a shared boundary reach it at the same time (both at their start, or both at
+// their end) while they run side by side on one XCD.  A reversed band produces the same u rows
+// (the vertical blend keeps its operand order), but each conv row then accumulates its below
+// taps first and its above taps last: the same products, summed in another order (fp32
+// rounding level; the bias still comes first).
+template <int OP>
 __global__ __launch_bounds__(F4_THREADS) __attribute__((amdgpu_waves_per_eu(F4_WPE)))
 void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
               const float* __restrict__ bias, __bf16* __restrict__ y, FusedGeom F) {
     constexpr int C = 3, O = 3;
-    constexpr bool UIN = MD == 1;                    // u rows = input rows
     constexpr int PD = F4_PD;
-    static_assert(PD >= 1 && PD <= 4, "raw ring: rows a2+2 .. a2+1+PD in flight in 6 slots");
-    constexpr int NLUT_MAX = (F4_RB > F4_RB_CONV ? F4_RB : F4_RB_CONV) + 2;
-    __shared__ float4 lut_all[F4_GW][NLUT_MAX];
-    // DMA: per wave 6 row slots of 3 x 512 B (plane c of rect row R at slot (R - s0 + 2) % 6,
-    // bytes c * 512 + 8 * lane = this lane's 4 columns); pairs of slots (0,1) (2,3) (4,5) are
-    // contiguous, so two rows are three 1-KiB LDS-DMA pieces
-    constexpr bool DMA = F4_DMA;
-    constexpr int RSLOT = 3 * 512;
-    __shared__ __attribute__((aligned(16))) unsigned char ring_all[DMA ? F4_GW : 1][DMA ? 6 * RSLOT : 16];
+    static_assert(PD >= 1 && PD <= 4, "raw ring: rows k+2 .. k+1+PD in flight in 6 slots");
+    constexpr int RB = F4_RB, NLUT = RB + 2;
+    __shared__ float4 lut_all[F4_GW][NLUT];
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4* const lut = lut_all[wslot];
-    const unsigned char* const ring = ring_all[DMA ? wslot : 0];
-    const unsigned ring_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)ring_all[DMA ? wslot : 0];
     const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
     const int ngrp = (F.nwin + F4_GW - 1) / F4_GW;
-    // block -> (window group, band, image): group fastest (F4_ORDER 0) or band fastest (1: the
-    // bands of one window group run side by side, sharing their 4 halo rows in L2)
-    // (2: group fastest, then image, then band: the waves resident together walk the same
-    // rows of many images)
+    // block -> (window group, band, image): group fastest (F4_ORDER 0) or band fastest (1)
     const int grp = (int)(F4_ORDER == 1 ? (blk / F.nband) % ngrp : blk % ngrp);
-    const int band = (int)(F4_ORDER == 1 ? blk % F.nband
-                           : F4_ORDER == 2 ? blk / ((int64_t)ngrp * F.B) : (blk / ngrp) % F.nband);
-    const int64_t b = F4_ORDER == 2 ? (blk / ngrp) % F.B : blk / ((int64_t)ngrp * F.nband);
-    if (band >= F.nband) return;
+    const int band = (int)(F4_ORDER == 1 ? blk % F.nband : (blk / ngrp) % F.nband);
+    const int64_t b = blk / ((int64_t)ngrp * F.nband);
     if (b >= F.B) return;                            // uniform per workgroup
     const int win = grp * F4_GW + wslot;             // may be >= nwin: runs, owns nothing
     const int W0 = win * F4_OWN - F4_HL;
     const int ce = W0 + 4 * lane;                    // columns ce .. ce + 3 (pairs A, B)
-    constexpr int RB = MD == 1 ? F4_RB_CONV : F4_RB, NLUT = RB + 2;
     const int s0 = band * RB;
     const int s1 = min(s0 + RB, F.h2);
+    const bool up = F4_REV && (band & 1) && s1 - s0 == RB;   // uniform
 
     // ---- row table (fp64 lattice math, geometry_np.py:440-486), as k_fused -------------
+    // entry e: u row s0 - 1 + e = {a, b, c}: u[r] = a x[r-1] + b x[r] + c x[r+1]
     for (int e = lane; e < NLUT; e += 64) {
         const int r = s0 - 1 + e;
         float4 t = {0.f, 0.f, 0.f, 0.f};
-        if (UIN) {
-            t.y = (r >= 0 && r < F.h) ? 1.f : 0.f;       // u row r = input row r; 0: padding row
-        } else if (F4_DIAG_NOFP64) {
-            t.x = 0.25f; t.y = 0.75f;
-        } else if (r >= 0 && r < F.h1) {
+        if (r >= 0 && r < F.h1) {
             const double i_ = axis_at(F.rxs, r) + (double)(F.h - 1) * 0.5;   // :440
             const int in = (int)i_;                                          // :444
             const double f = i_ - (double)(float)in;                         // :448
@@ -147,8 +119,8 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    int rc = 0;
-    if (!UIN) {
+    int rc;
+    {
         bool has_a = false, has_c = false;
         for (int e = lane; e < NLUT; e += 64) {
             const float4 t = lut[e];
@@ -170,9 +142,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             float* wr = s ? wo[k] : we[k];
             wr[0] = wr[1] = wr[2] = 0.f;
             const int q = ce + 2 * k + s;
-            if (F4_DIAG_NOFP64) {
-                wr[0] = 0.25f; wr[1] = 0.75f;
-            } else if (!UIN && q >= 0 && q < F.w1) {
+            if (q >= 0 && q < F.w1) {
                 const double j_ = axis_at(F.rys, q) + (double)(F.w - 1) * 0.5;   // :441
                 const int jn = (int)j_;
                 const double jf = j_ - (double)(float)jn;
@@ -191,7 +161,6 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     const bool any_r = __builtin_amdgcn_ballot_w64(we[0][2] != 0.f || wo[0][2] != 0.f ||
                                                    we[1][2] != 0.f || wo[1][2] != 0.f) != 0;
     const int cd = !any_r ? 1 : (!any_l ? 2 : 0);
-    const bool colin = ce >= 0 && ce < F.w;          // MD 1: the lane's input columns (w % 4 == 0)
 
     // owned lanes 2 .. 61 (w2 % 4 == 0: a lane is wholly inside or outside the raster)
     const bool own = lane >= F4_HL / 4 && lane < (F4_HL + F4_OWN) / 4 && ce >= 0 && ce < F.w2 &&
@@ -208,52 +177,12 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     const unsigned yoff = own ? (unsigned)ce * 2u : 0x80000000u;
     const unsigned xplane = (unsigned)(cstride * 2), yplane = (unsigned)(ostride * 2);
     const unsigned xrow = (unsigned)F.w * 2u, yrow = (unsigned)F.w2 * 2u;
-    auto row_off = [&](int k) -> unsigned {
+    auto row_off = [&](int r) -> unsigned {
         if (F4_NOMEM == 1 || F4_NOMEM == 2) return 0u;
-        return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(k, 0), F.h - 1) * xrow));
-    };
-    // DMA: piece j of a row pair (A, B) is 1 KiB: half-wave h (lanes 32 h .. 32 h + 31) moves the
-    // 512-B plane row 2 j + h of [A0 A1 A2 B0 B1 B2], lane l the 16 B of columns W0 + 8 (l % 32)
-    // .. + 7; columns left or right of the raster are out of the buffer range (zeros)
-    const int dgc = W0 + 8 * (lane & 31);
-    const unsigned dcol = (dgc >= 0 && dgc < F.w) ? (unsigned)dgc * 2u : 0x80000000u;
-    const bool dhi = lane >= 32;
-    const unsigned dv0 = dcol + (dhi ? xplane : 0u);              // A0 | A1   (+ row A)
-    const unsigned dv1 = dcol + (dhi ? 0u : 2u * xplane);         // A2 | B0   (+ row A, hi: + B - A)
-    const unsigned dv2 = dcol + (dhi ? 2u * xplane : xplane);     // B1 | B2   (+ row B)
-    // rows R, R + 1 into the slot pair starting at even slot PS (inline asm: hipcc does not see
-    // these loads, so it adds no vmcnt(0) before LDS reads; the waits are counted in step())
-    auto dma_pair = [&](int R, auto PSc) {
-        constexpr int PS = decltype(PSc)::value;
-        const unsigned rA = row_off(R), rB = row_off(R + 1);
-        const unsigned v1 = dv1 + (dhi ? rB - rA : 0u);
-        const unsigned l0 = (unsigned)__builtin_amdgcn_readfirstlane((int)(ring_lds + PS * RSLOT));
-        const unsigned l1 = l0 + 1024u, l2 = l0 + 2048u;
-        unsigned keep;
-        const unsigned a0 = dv0, a2 = dv2;
-        const __amdgpu_buffer_rsrc_t rs = xrs;
-        asm volatile("s_mov_b32 %0, m0\n\t"
-                     "s_mov_b32 m0, %4\n\t"
-                     "s_nop 0\n\t"
-                     "buffer_load_dwordx4 %1, %7, %8 offen lds\n\t"
-                     "s_mov_b32 m0, %5\n\t"
-                     "s_nop 0\n\t"
-                     "buffer_load_dwordx4 %2, %7, %8 offen lds\n\t"
-                     "s_mov_b32 m0, %6\n\t"
-                     "s_nop 0\n\t"
-                     "buffer_load_dwordx4 %3, %7, %9 offen lds\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(a0), "v"(v1), "v"(a2), "s"(l0), "s"(l1), "s"(l2), "s"(rs), "s"(rA), "s"(rB)
-                     : "memory");
-    };
-    auto dma_read = [&](int R, f4_u2 (&r)[3]) {
-        const unsigned char* const src = ring + fu_mod(R - s0 + 2, 6) * RSLOT + 8 * lane;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) r[c] = *reinterpret_cast<const f4_u2*>(src + c * 512);
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(r, 0), F.h - 1) * xrow));
     };
 
-    // ---- weights (21 pairs in SGPRs, the rest opaque VGPR pairs) and bias ---------------
+    // ---- weights (29 pairs in SGPRs, the rest opaque VGPR pairs) and bias ---------------
     int vz = 0;
     asm volatile("" : "+v"(vz));
     constexpr int NW = O * C * 7, NWP = (NW + 1) / 2;
@@ -269,7 +198,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     }
     float bv[O];
 #pragma unroll
-    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] * (MD == 0 ? 0.75f : 1.f) : 0.f;
+    for (int o = 0; o < O; ++o) bv[o] = bias ? bias[o + vz] * 0.75f : 0.f;
     fu_f2 bvp[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -285,18 +214,26 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     unsigned hi16 = 0xffff0000u;
     asm volatile("" : "+v"(hi16));
 
-    auto run = [&](auto CDc, auto RCc) {
+    // A band is walked in steps k = 0 .. s1 - s0 - 1 over output rows row(k): downwards
+    // (row(k) = s0 + k) or, UP, upwards (row(k) = s1 - 1 - k).  Rect row / u row / conv row
+    // row(k) lives in ring slot k mod 6 / k mod 3, so the slots and the row parities are
+    // compile-time per step of a 6-step block in both directions.
+    auto run = [&](auto CDc, auto RCc, auto UPc) {
         constexpr int CD = decltype(CDc)::value;
         constexpr int RC = decltype(RCc)::value;
-        f4_u2 raw[6][C];                    // rect rows in flight, slot (row - s0) % 6
-        fu_f2 XA[3][C], XB[3][C];           // rect rows as f32 pairs A / B, slot (row - s0) % 3
-        fu_f2 ZA[3][O], ZB[3][O];           // conv rows being accumulated, slot (row - s0) % 3
+        constexpr bool UP = decltype(UPc)::value;
+        auto row = [&](int k) { return UP ? s1 - 1 - k : s0 + k; };
+        // row-table entry of u row row(j)
+        auto lut_e = [&](int j) { return UP ? RB - j : j + 1; };
+        f4_u2 raw[6][C];                    // rect rows in flight, slot k % 6
+        fu_f2 XA[3][C], XB[3][C];           // rect rows as f32 pairs A / B, slot k % 3
+        fu_f2 ZA[3][O], ZB[3][O];           // conv rows being accumulated, slot k % 3
 
-        auto issue = [&](auto SLc, int k) {
+        auto issue = [&](auto SLc, int r) {
             constexpr int SL = decltype(SLc)::value;
-            const unsigned so = row_off(k);
+            const unsigned so = row_off(r);
 #pragma unroll
-            for (int c = 0; c < C; ++c) raw[SL][c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, xoff, so + c * xplane, F4_LAUX);
+            for (int c = 0; c < C; ++c) raw[SL][c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, xoff, so + c * xplane, 0);
         };
         auto convert = [&](auto RSc, auto XSc) {
             constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
@@ -304,33 +241,29 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             for (int c = 0; c < C; ++c) f4_unpack(raw[RS][c], XA[XS][c], XB[XS][c], hi16);
         };
 
-        // u row r (= s0 + PH + 1) from rect rows r-1, r, r+1 (XP slots PH, PH+1, PH+2 mod 3),
-        // scattered into conv rows r+1 (above; slot PH+2, started with the bias), r (centre;
-        // slot PH+1) and r-1 (below; slot PH)
+        // u row row(j), j = PH + 1, from rect rows row(PH), row(PH+1), row(PH+2) (slots S0, S1,
+        // S2), scattered into conv rows row(PH+2) (started here with the bias: slot S2), row(PH+1)
+        // (centre: S1) and row(PH) (completed here: S0).  Downwards the started row is the one
+        // below (u row = its 'above' row: taps 0, 1), upwards the one above (taps 5, 6).
         auto urow = [&](auto PHc, float4 L, auto CENc, auto BELc) {
             constexpr int PH = decltype(PHc)::value;
             constexpr bool CEN = decltype(CENc)::value, BEL = decltype(BELc)::value;
             constexpr int S0 = fu_mod(PH, 3), S1 = fu_mod(PH + 1, 3), S2 = fu_mod(PH + 2, 3);
-            constexpr int PB = fu_mod(PH, 2), PC = 1 - PB;
+            // slots of rect rows r - 1 and r + 1 (r = row(PH + 1))
+            constexpr int XM = UP ? S2 : S0, XQ = UP ? S0 : S2;
+            // parity of the started / completed rows (row(PH) and row(PH + 2)); s0 and, for an
+            // UP band, s1 are even
+            constexpr int PB = UP ? fu_mod(PH + 1, 2) : fu_mod(PH, 2), PC = 1 - PB;
+            constexpr int TN = UP ? 5 : 0, TD = UP ? 0 : 5;   // first tap of started / completed row
             const fu_f2 Lxy = {L.x, L.y}, Lzw = {L.z, L.w};
             fu_sfor<0, C>([&](auto Cc) {
                 constexpr int c = decltype(Cc)::value;
                 float ue[2], uo[2];
-                if constexpr (UIN) {                // MD 1: u = input row r, 0 outside (padding 1)
-                    if constexpr (RC == 1) {        // interior band and window: no selects
-                        ue[0] = XA[S1][c].x; uo[0] = XA[S1][c].y;
-                        ue[1] = XB[S1][c].x; uo[1] = XB[S1][c].y;
-                    } else {
-                        const bool in_ = colin && L.y != 0.f;
-                        ue[0] = in_ ? XA[S1][c].x : 0.f; uo[0] = in_ ? XA[S1][c].y : 0.f;
-                        ue[1] = in_ ? XB[S1][c].x : 0.f; uo[1] = in_ ? XB[S1][c].y : 0.f;
-                    }
-                } else {
-                // vertical blend, packed (k_fused FU_VPK), for both pairs
+                // vertical blend, packed (k_fused FU_VPK), for both pairs: a x[r-1] + b x[r] + c x[r+1]
                 auto vblend = [&](const fu_f2 (&X)[3][C]) {
-                    if constexpr (RC == 1) return fu_pfma<1, false>(Lxy, X[S1][c], fu_pmul<0>(Lxy, X[S0][c]));
-                    else if constexpr (RC == 2) return fu_pfma<0, false>(Lzw, X[S2][c], fu_pmul<1>(Lxy, X[S1][c]));
-                    else return fu_pfma<0, false>(Lzw, X[S2][c], fu_pfma<1, false>(Lxy, X[S1][c], fu_pmul<0>(Lxy, X[S0][c])));
+                    if constexpr (RC == 1) return fu_pfma<1, false>(Lxy, X[S1][c], fu_pmul<0>(Lxy, X[XM][c]));
+                    else if constexpr (RC == 2) return fu_pfma<0, false>(Lzw, X[XQ][c], fu_pmul<1>(Lxy, X[S1][c]));
+                    else return fu_pfma<0, false>(Lzw, X[XQ][c], fu_pfma<1, false>(Lxy, X[S1][c], fu_pmul<0>(Lxy, X[XM][c])));
                 };
                 const fu_f2 VA = vblend(XA), VB = vblend(XB);
                 // horizontal blend: columns ce .. ce+3 = VA.x VA.y VB.x VB.y; the lane's left
@@ -352,7 +285,6 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
                     ue[1] = fmaf(we[1][2], VB.y, fmaf(we[1][1], VB.x, we[1][0] * VA.y));
                     uo[1] = fmaf(wo[1][2], nx, fmaf(wo[1][1], VB.y, wo[1][0] * VB.x));
                 }
-                }
                 // the stencil's column-shifted pairs (u[ce+s], u[ce+1+s]) for both pairs:
                 // s = 0: own; s = 1: (uo_k, ue_{k+1}); s = -1: (uo_{k-1}, ue_k); s = 2: pair k+1
                 const float nue = f_next(ue[0]);                 // next lane's u[ce + 4]
@@ -372,43 +304,43 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
                         zA = fu_pfma<j & 1, WS>(wkp[j >> 1], aA, zA);
                         zB = fu_pfma<j & 1, WS>(wkp[j >> 1], aB, zB);
                     };
-                    if constexpr (c == 0) {       // the first tap of conv row r+1 adds the bias
-                        constexpr bool WS = (j0 >> 1) < NWS;
-                        const int s = fu_tap_shift(0, PB, OP);
+                    if constexpr (c == 0) {       // the first tap of the started row adds the bias
+                        constexpr int jb = j0 + TN;
+                        constexpr bool WS = (jb >> 1) < NWS;
+                        const int s = fu_tap_shift(TN, PB, OP);
                         const fu_f2 aA = s == -1 ? Um[0] : (s == 0 ? U0[0] : (s == 1 ? U1[0] : U2[0]));
                         const fu_f2 aB = s == -1 ? Um[1] : (s == 0 ? U0[1] : (s == 1 ? U1[1] : U2[1]));
-                        ZA[S2][o] = fu_pfma_b<j0 & 1, o & 1, WS>(wkp[j0 >> 1], aA, bvp[o >> 1]);
-                        ZB[S2][o] = fu_pfma_b<j0 & 1, o & 1, WS>(wkp[j0 >> 1], aB, bvp[o >> 1]);
+                        ZA[S2][o] = fu_pfma_b<jb & 1, o & 1, WS>(wkp[jb >> 1], aA, bvp[o >> 1]);
+                        ZB[S2][o] = fu_pfma_b<jb & 1, o & 1, WS>(wkp[jb >> 1], aB, bvp[o >> 1]);
                     } else {
-                        tapk(IC<0>{}, ZA[S2][o], ZB[S2][o], PB);
+                        tapk(IC<TN>{}, ZA[S2][o], ZB[S2][o], PB);
                     }
-                    tapk(IC<1>{}, ZA[S2][o], ZB[S2][o], PB);
+                    tapk(IC<TN + 1>{}, ZA[S2][o], ZB[S2][o], PB);
                     if constexpr (CEN) {
                         tapk(IC<2>{}, ZA[S1][o], ZB[S1][o], PC);
                         tapk(IC<3>{}, ZA[S1][o], ZB[S1][o], PC);
                         tapk(IC<4>{}, ZA[S1][o], ZB[S1][o], PC);
                     }
-                    if constexpr (BEL && !F4_DIAG_NOBEL) {
-                        tapk(IC<5>{}, ZA[S0][o], ZB[S0][o], PB);
-                        tapk(IC<6>{}, ZA[S0][o], ZB[S0][o], PB);
+                    if constexpr (BEL) {
+                        tapk(IC<TD>{}, ZA[S0][o], ZB[S0][o], PB);
+                        tapk(IC<TD + 1>{}, ZA[S0][o], ZB[S0][o], PB);
                     }
                 });
             });
         };
 
-        // conv row a2 (slot PH % 3, parity PH % 2) -> output row a2 (the folded same-size h2r:
-        // even rows z'[b] + z'[b+1] / 3, odd rows z'[b-1] / 3 + z'[b], geometry_np.py:347-354)
-        auto out_row = [&](auto PHc, int a2) {
+        // conv row row(PH) (slot PH % 3) -> output row row(PH) (the folded same-size h2r: even
+        // rows z'[b] + z'[b+1] / 3, odd rows z'[b-1] / 3 + z'[b], geometry_np.py:347-354)
+        auto out_row = [&](auto PHc, int k) {
             constexpr int PH = decltype(PHc)::value;
             constexpr int S0 = PH % 3;
-            const unsigned so = (F4_NOMEM == 1 || F4_NOMEM == 3) ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)a2 * yrow));
+            constexpr int PAR = UP ? (PH + 1) & 1 : PH & 1;
+            const unsigned so = (F4_NOMEM == 1 || F4_NOMEM == 3) ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)row(k) * yrow));
 #pragma unroll
             for (int o = 0; o < O; ++o) {
                 const fu_f2 zA = ZA[S0][o], zB = ZB[S0][o];
                 float o0, o1, o2, o3;
-                if constexpr (MD == 1) {            // HexConv2d output row as is
-                    o0 = zA.x; o1 = zA.y; o2 = zB.x; o3 = zB.y;
-                } else if constexpr ((PH & 1) == 0) {
+                if constexpr (PAR == 0) {
                     o0 = fmaf(c13, zA.y, zA.x);
                     o1 = fmaf(c13, zB.x, zA.y);
                     o2 = fmaf(c13, zB.y, zB.x);
@@ -422,90 +354,54 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
                 typedef __bf16 t2v __attribute__((ext_vector_type(2)));
                 const f4_u2 v = {__builtin_bit_cast(unsigned, t2v{(__bf16)o0, (__bf16)o1}),
                                  __builtin_bit_cast(unsigned, t2v{(__bf16)o2, (__bf16)o3})};
-                __builtin_amdgcn_raw_buffer_store_b64(v, yrs, yoff, so + o * yplane, F4_SAUX);
+                __builtin_amdgcn_raw_buffer_store_b64(v, yrs, yoff, so + o * yplane, 0);
             }
         };
 
-        // ---- prologue: u rows s0-1 and s0 -----------------------------------------------
-        if constexpr (DMA) {
-            dma_pair(s0 - 2, IC<0>{});
-            dma_pair(s0, IC<2>{});
-            dma_pair(s0 + 2, IC<4>{});
-            __builtin_amdgcn_s_waitcnt(0x0f70);                         // vmcnt(0)
-            asm volatile("" ::: "memory");
-            f4_u2 t0[C], t1[C], t2[C];
-            dma_read(s0 - 2, t0);
-            dma_read(s0 - 1, t1);
-            dma_read(s0, t2);
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                f4_unpack(t0[c], XA[1][c], XB[1][c], hi16);   // row s0-2 -> slot 1
-                f4_unpack(t1[c], XA[2][c], XB[2][c], hi16);   // row s0-1 -> slot 2
-                f4_unpack(t2[c], XA[0][c], XB[0][c], hi16);   // row s0   -> slot 0
-            }
-            urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});
-            dma_read(s0 + 1, t0);
-#pragma unroll
-            for (int c = 0; c < C; ++c) f4_unpack(t0[c], XA[1][c], XB[1][c], hi16);   // row s0+1
-            urow(IC<-1>{}, lut[1], std::true_type{}, std::false_type{});
-        } else {
+        // ---- prologue: u rows row(-1) and row(0) ----------------------------------------
         {
             f4_u2 t0[C], t1[C], t2[C];
-            const unsigned o0 = row_off(s0 - 2), o1 = row_off(s0 - 1), o2 = row_off(s0);
+            const unsigned o0 = row_off(row(-2)), o1 = row_off(row(-1)), o2 = row_off(row(0));
 #pragma unroll
             for (int c = 0; c < C; ++c) {
                 t0[c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, xoff, o0 + c * xplane, 0);
                 t1[c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, xoff, o1 + c * xplane, 0);
                 t2[c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, xoff, o2 + c * xplane, 0);
             }
-            issue(IC<1>{}, s0 + 1);
+            issue(IC<1>{}, row(1));
 #pragma unroll
-            for (int i = 0; i < PD; ++i) {          // ring: rect rows s0+2 .. s0+1+PD
-                if (i == 0) issue(IC<2>{}, s0 + 2);
-                if (i == 1) issue(IC<3>{}, s0 + 3);
-                if (i == 2) issue(IC<4>{}, s0 + 4);
-                if (i == 3) issue(IC<5>{}, s0 + 5);
+            for (int i = 0; i < PD; ++i) {          // ring: rect rows row(2) .. row(1 + PD)
+                if (i == 0) issue(IC<2>{}, row(2));
+                if (i == 1) issue(IC<3>{}, row(3));
+                if (i == 2) issue(IC<4>{}, row(4));
+                if (i == 3) issue(IC<5>{}, row(5));
             }
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                f4_unpack(t0[c], XA[1][c], XB[1][c], hi16);   // row s0-2 -> slot 1
-                f4_unpack(t1[c], XA[2][c], XB[2][c], hi16);   // row s0-1 -> slot 2
-                f4_unpack(t2[c], XA[0][c], XB[0][c], hi16);   // row s0   -> slot 0
+                f4_unpack(t0[c], XA[1][c], XB[1][c], hi16);   // row(-2) -> slot 1
+                f4_unpack(t1[c], XA[2][c], XB[2][c], hi16);   // row(-1) -> slot 2
+                f4_unpack(t2[c], XA[0][c], XB[0][c], hi16);   // row(0)  -> slot 0
             }
         }
-        urow(IC<-2>{}, lut[0], std::false_type{}, std::false_type{});   // u row s0-1: above only
-        convert(IC<1>{}, IC<1>{});                                      // row s0+1 -> slot 1
-        urow(IC<-1>{}, lut[1], std::true_type{}, std::false_type{});    // u row s0: above, centre
-        __builtin_amdgcn_s_waitcnt(0x0f70);                             // vmcnt(0)
-        }
+        urow(IC<-2>{}, lut[lut_e(-1)], std::false_type{}, std::false_type{});   // u row(-1): start only
+        convert(IC<1>{}, IC<1>{});                                              // row(1) -> slot 1
+        urow(IC<-1>{}, lut[lut_e(0)], std::true_type{}, std::false_type{});     // u row(0): start, centre
+        __builtin_amdgcn_s_waitcnt(0x0f70);                                     // vmcnt(0)
 
         // ---- main loop -----------------------------------------------------------------
-        float4 lnext = lut[2];
-        auto step = [&](auto PHc, int a2) {
+        const int n = s1 - s0;
+        float4 lnext = lut[lut_e(1)];
+        auto step = [&](auto PHc, int k) {
             constexpr int PH = decltype(PHc)::value;
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (DMA) {
-                // rect row a2+2 landed once at most the operations issued after its last piece
-                // are outstanding (vmcnt counts LDS-DMA and stores together, in issue order):
-                // even steps read the first row of the pair issued two steps back (after its
-                // piece 1: piece 2 + 2 x 3 stores), odd steps the second row of the pair issued
-                // three steps back (after piece 2: 3 x 3 stores + one pair); the prologue drains
-                constexpr int N = (PH & 1) ? 12 : 7;
-                __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf));
-                asm volatile("" ::: "memory");
-                f4_u2 r[C];
-                dma_read(a2 + 2, r);
-#pragma unroll
-                for (int c = 0; c < C; ++c) f4_unpack(r[c], XA[(PH + 2) % 3][c], XB[(PH + 2) % 3][c], hi16);
-                if constexpr ((PH & 1) == 0) dma_pair(a2 + 4, IC<PH % 6>{});   // rows a2+4, a2+5
-            } else {
-            convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row a2+2
-            issue(IC<(PH + 2 + PD) % 6>{}, a2 + 2 + PD);
-            }
+            convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row row(k+2)
+            // (past the band's last halo row the load repeats that row: an L2 hit, not a
+            // 31st row from HBM)
+            issue(IC<(PH + 2 + PD) % 6>{}, row(min(k + 2 + PD, n + 1)));
             const float4 L = lnext;
-            lnext = lut[min(a2 - s0 + 3, NLUT - 1)];
-            urow(PHc, L, std::true_type{}, std::true_type{});           // u row a2+1
-            out_row(PHc, a2);
+            lnext = lut[min(max(lut_e(k + 2), 0), NLUT - 1)];
+            urow(PHc, L, std::true_type{}, std::true_type{});           // u row row(k+1)
+            out_row(PHc, k);
         };
         auto block6 = [&](int base) {
             step(IC<0>{}, base);
@@ -515,39 +411,33 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             step(IC<4>{}, base + 4);
             step(IC<5>{}, base + 5);
         };
-        auto tail = [&](int base) {
-            if (base >= s1) return;
-            step(IC<0>{}, base);
-            if (base + 1 < s1) {
-                step(IC<1>{}, base + 1);
-                if (base + 2 < s1) {
-                    step(IC<2>{}, base + 2);
-                    if (base + 3 < s1) {
-                        step(IC<3>{}, base + 3);
-                        if (base + 4 < s1) step(IC<4>{}, base + 4);
+        int base = 0;
+        for (; base + 6 <= n; base += 6) block6(base);
+        if constexpr (!UP) {                            // (UP bands are whole 6-step blocks)
+            if (base < n) {
+                step(IC<0>{}, base);
+                if (base + 1 < n) {
+                    step(IC<1>{}, base + 1);
+                    if (base + 2 < n) {
+                        step(IC<2>{}, base + 2);
+                        if (base + 3 < n) {
+                            step(IC<3>{}, base + 3);
+                            if (base + 4 < n) step(IC<4>{}, base + 4);
+                        }
                     }
                 }
             }
-        };
-        int base = s0;
-        for (; base + 6 <= s1; base += 6) block6(base);
-        tail(base);
-        if constexpr (DMA) __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): no LDS-DMA in flight at exit
+        }
     };
-    if constexpr (UIN) {
-        (void)cd; (void)rc;
-        // every u row of the band (s0 - 1 .. s1) and every lane's columns inside the input: the
-        // padding selects drop out (RC 1 marks that loop for MD 1)
-        const bool inner = s0 >= 1 && s1 + 1 <= F.h && __builtin_amdgcn_ballot_w64(!colin) == 0;
-        if (inner) run(IC<0>{}, IC<1>{});
-        else run(IC<0>{}, IC<0>{});
-        return;
-    }
-    if (cd == 1 && rc == 1) run(IC<1>{}, IC<1>{});
-    else if (cd == 1 && rc == 2) run(IC<1>{}, IC<2>{});
-    else if (cd == 2 && rc == 1) run(IC<2>{}, IC<1>{});
-    else if (cd == 2 && rc == 2) run(IC<2>{}, IC<2>{});
-    else run(IC<0>{}, IC<0>{});
+    auto dir = [&](auto CDc, auto RCc) {
+        if (F4_REV && up) run(CDc, RCc, std::true_type{});
+        else run(CDc, RCc, std::false_type{});
+    };
+    if (cd == 1 && rc == 1) dir(IC<1>{}, IC<1>{});
+    else if (cd == 1 && rc == 2) dir(IC<1>{}, IC<2>{});
+    else if (cd == 2 && rc == 1) dir(IC<2>{}, IC<1>{});
+    else if (cd == 2 && rc == 2) dir(IC<2>{}, IC<2>{});
+    else dir(IC<0>{}, IC<0>{});
 }
 
 // The 4-column kernel for a call fused_try has validated (same-size lattice, padding 1,
@@ -564,36 +454,9 @@ int fused4_try(const void* x, const float* k, const float* bias, void* y, int x_
     if (blocks > INT_MAX) return HG_EUNSUP;
     const dim3 grid((unsigned)blocks), blk(F4_THREADS);
     if (op)
-        hipLaunchKernelGGL((k_fused4<1, 0>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
+        hipLaunchKernelGGL((k_fused4<1>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
     else
-        hipLaunchKernelGGL((k_fused4<0, 0>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
-    return launch_status();
-}
-
-// HexConv2d alone (radius 2, stride 1, padding 1, pad value 0, no epilogue) on the 4-column
-// kernel (MD 1): bf16 in and out, C = O = 3, groups 1, w a multiple of 4; HG_EUNSUP otherwise
-// (the caller runs k_fused MD 1).  op = tap column class at padding 1 ((off + 1) & 1).
-int fconv4_try(const void* x, const float* k, const float* bias, void* y, int x_dtype, int y_dtype,
-               int64_t batch, int C, int O, int G, int64_t h, int64_t w, int op, hipStream_t st) {
-    // Opt-in (HYGRID_FCONV4=1): at 18-row bands 1.7 % SLOWER than k_fused MD 1 on the 4K bf16
-    // b128 conv (2.710 vs 2.664 ms, profiles/r05/fconv4_ab.txt); bit-identical to it.
-    if (!env_is("HYGRID_FCONV4", "1")) return HG_EUNSUP;
-    if (x_dtype != HG_BF16 || y_dtype != HG_BF16 || C != 3 || O != 3 || G != 1) return HG_EUNSUP;
-    if ((w % 4) || w < 4 || h < 1 || batch < 1) return HG_EUNSUP;
-    if (3 * h * w * 2 >= ((int64_t)1 << 31)) return HG_EUNSUP;   // 32-bit offsets per image
-    FusedGeom F = {};
-    F.B = batch;
-    F.h = F.h1 = F.h2 = (int)h;
-    F.w = F.w1 = F.w2 = (int)w;
-    F.nwin = (int)((w + F4_OWN - 1) / F4_OWN);
-    F.nband = (int)((h + F4_RB_CONV - 1) / F4_RB_CONV);
-    const int64_t blocks = F.B * (int64_t)F.nband * ((F.nwin + F4_GW - 1) / F4_GW);
-    if (blocks > INT_MAX) return HG_EUNSUP;
-    const dim3 grid((unsigned)blocks), blk(F4_THREADS);
-    if (op)
-        hipLaunchKernelGGL((k_fused4<1, 1>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
-    else
-        hipLaunchKernelGGL((k_fused4<0, 1>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
+        hipLaunchKernelGGL((k_fused4<0>), grid, blk, 0, st, (const __bf16*)x, k, bias, (__bf16*)y, F);
     return launch_status();
 }
 
@@ -604,12 +467,6 @@ namespace hg {
 // place edge inputs from it)
 void fused4_layout(int* band_rows, int* win_own, int* win_halo) {
     *band_rows = F4_RB;
-    *win_own = F4_OWN;
-    *win_halo = F4_HL;
-}
-// the same for the HexConv2d mode (hg_fused_layout(8, ...))
-void fconv4_layout(int* band_rows, int* win_own, int* win_halo) {
-    *band_rows = F4_RB_CONV;
     *win_own = F4_OWN;
     *win_halo = F4_HL;
 }

@@ -35,9 +35,6 @@ static int fconv_channels(const void* x, const float* k, const float* b, void* y
     return HG_EUNSUP;
 }
 
-int fconv4_try(const void* x, const float* k, const float* bias, void* y, int x_dtype, int y_dtype,
-               int64_t batch, int C, int O, int G, int64_t h, int64_t w, int op, hipStream_t st);
-
 int fused_conv_try(const void* x, const float* kernel, const float* bias, void* y, int x_dtype,
                    int y_dtype, int64_t batch, int C, int O, int G, int64_t h, int64_t w,
                    int padding, int off, double pad_value, bool epilogue, hipStream_t st) {
@@ -53,10 +50,6 @@ int fused_conv_try(const void* x, const float* kernel, const float* bias, void* 
     F.nwin = (int)((w + FU_OWN - 1) / FU_OWN);
     F.nband = (int)((h + fu_rb(1) - 1) / fu_rb(1));
     const int op = (off + padding) & 1;
-    {   // fused4.hip: the 4-column kernel (bf16, C = O = 3, widths a multiple of 4)
-        const int rc4 = fconv4_try(x, kernel, bias, y, x_dtype, y_dtype, batch, C, O, G, h, w, op, st);
-        if (rc4 != HG_EUNSUP) return rc4;
-    }
     if (x_dtype == HG_BF16 && y_dtype == HG_BF16)
         return fconv_channels<__bf16, __bf16>(x, kernel, bias, y, F, C, O, G, op, st);
     if (x_dtype == HG_BF16 && y_dtype == HG_F32)

@@ -699,9 +699,8 @@ void k_fused(const Tin* __restrict__ x,
                 const unsigned* const src =
                     dstg + ((R & 1) * O + dpl) * DP * 256 + dpp * 240 + 4 * min(lane, 59);
                 if (!dedge) {
-                    typedef unsigned u4v __attribute__((ext_vector_type(4)));
-                    const u4v q = *reinterpret_cast<const u4v*>(src);
-                    __builtin_amdgcn_raw_buffer_store_b128(q, yrs, valid ? dsoff : 0x80000000u, so, 0);
+                    const hg_u4v q = *reinterpret_cast<const hg_u4v*>(src);
+                    hg_store_b128(q, yrs, valid ? dsoff : 0x80000000u, so);
                 } else {   // the row end crosses a 16-B piece: dword stores, column-checked
     #pragma unroll
                     for (int i = 0; i < 4; ++i) {

@@ -126,8 +126,7 @@ __device__ __forceinline__ void st_store(const float* v, __amdgpu_buffer_rsrc_t 
     } else if constexpr (CPL == 4) {
         typedef float f4 __attribute__((ext_vector_type(4)));
         const f4 e = {v[0], v[1], v[2], v[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(typename Vec4Of<T>::type, e), rs,
-                                               voff, soff, 0);
+        hg_store_b128(__builtin_bit_cast(hg_u4v, e), rs, voff, soff);
     } else {
         typedef float f2 __attribute__((ext_vector_type(2)));
         typedef unsigned u2 __attribute__((ext_vector_type(2)));

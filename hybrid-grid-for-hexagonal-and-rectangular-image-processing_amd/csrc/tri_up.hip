@@ -110,21 +110,17 @@ template <> struct UInt<1> { using T = uint8_t; };
 template <> struct UInt<2> { using T = unsigned short; };
 template <> struct UInt<4> { using T = unsigned; };
 
-// One lane's K-sample store of `bytes` = K * sizeof(Tout) bytes from the packed words v.
-// 12/16-byte stores take the row offset in the VGPR offset and soffset 0: with an SGPR soffset
-// the compiler puts no wait state between the store and a VALU write of its data registers,
-// and the MI355X then stored the overwritten value (bf16 -> f32 rows, r05;
-// tools/scan_store_hazard.py finds the pattern in device assembly).
+// One lane's K-sample store of `bytes` = K * sizeof(Tout) bytes from the packed words v
+// (16-byte stores: hg_store_b128, soffset 0 — the store-data hazard of round 5, common.h).
 template <int BYTES>
 __device__ __forceinline__ void tu_store(const unsigned (&v)[4], __amdgpu_buffer_rsrc_t rs, unsigned vo,
                                          unsigned so) {
     typedef unsigned u2v __attribute__((ext_vector_type(2)));
-    typedef unsigned u4v __attribute__((ext_vector_type(4)));
     if constexpr (BYTES == 1) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v[0], rs, vo, so, 0);
     else if constexpr (BYTES == 2) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v[0], rs, vo, so, 0);
     else if constexpr (BYTES == 4) __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, vo, so, 0);
     else if constexpr (BYTES == 8) __builtin_amdgcn_raw_buffer_store_b64(u2v{v[0], v[1]}, rs, vo, so, 0);
-    else __builtin_amdgcn_raw_buffer_store_b128(u4v{v[0], v[1], v[2], v[3]}, rs, vo + so, 0, 0);
+    else hg_store_b128(hg_u4v{v[0], v[1], v[2], v[3]}, rs, vo, so);
 }
 
 template <typename T> __device__ __forceinline__ float tu_f32(unsigned bits) {

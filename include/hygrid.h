@@ -71,11 +71,9 @@ const char* hg_build_digest(void);
 
 /* Work decomposition of the streaming fused kernel for mode md (0: hg_pipeline_r2h_conv_h2r,
  * 1: its HexConv2d mode, 2: hg_pipeline_r2h_h2r; 6: mode 0's four-column variant that runs
- * bf16 C = O = 3 calls with widths a multiple of 4; 7: mode 2's four-column variant that runs
- * calls with widths a multiple of 4 (opt-in, HYGRID_RT4=1); 8: mode 1's four-column variant that
- * runs bf16 C = O = 3 calls with widths a multiple of 4): output rows per band, owned columns per
- * window and the window's left halo.  Host-only; for tests that place inputs at band / window
- * edges. */
+ * bf16 C = O = 3 calls with widths a multiple of 4): output rows per band, owned columns per
+ * window and the window's left halo; HG_EINVAL for any other md.  Host-only; for tests that
+ * place inputs at band / window edges. */
 int hg_fused_layout(int md, int* band_rows, int* win_own, int* win_halo);
 
 /* rect -> hex lattice resample.

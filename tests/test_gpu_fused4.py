@@ -2,9 +2,13 @@
 (csrc/fused4.hip, k_fused4: bf16 in and out, C = O = 3, widths a multiple of 4 -- the
 headline's launch).  It evaluates the two-column kernel's (k_fused MD 0) products and sums per
 output in the same order (vertical and horizontal r2h blends, the 7 packed taps per conv row in
-tap order, the folded h2r), so its bf16 output is asserted BIT-IDENTICAL to the two-column
-kernel (HYGRID_FUSED4=0), NaN / Inf included, at band and window edges placed from
-hg_fused_layout(6); and within one bf16 rounding of the fp64 oracle chain."""
+tap order, the folded h2r), so on the bands it walks downwards its bf16 output is asserted
+BIT-IDENTICAL to the two-column kernel (HYGRID_FUSED4=0), NaN / Inf included, at band and window
+edges placed from hg_fused_layout(6); and within one bf16 rounding of the fp64 oracle chain.
+Round 6: odd full bands walk upwards (F4_REV, shared halo rows read together), where a conv row
+sums its below taps before its above taps: the same products in another order, so those rows
+are asserted within one bf16 step of the two-column kernel instead (and the oracle check holds
+for every row)."""
 import numpy as np
 import pytest
 import torch
@@ -43,10 +47,34 @@ def _oracle(x, conv):
     return O.hex_to_rect(c, None, 1)
 
 
-def _same(a, b):
+def _up_rows(H):
+    """Rows of the bands k_fused4 walks upwards: odd bands of the full band length."""
+    rows = _abi.fused_layout(6)[0]
+    up = torch.zeros(H, dtype=torch.bool)
+    for k in range(1, H // rows, 2):
+        if (k + 1) * rows <= H:
+            up[k * rows:(k + 1) * rows] = True
+    return up
+
+
+def _same(a, b, mask=None):
+    """Bit-identical outside the upward bands; within one bf16 step inside them (the same
+    products summed in another order can tip a rounding).  mask: (H, W) outputs to compare."""
     assert a.shape == b.shape and a.dtype == b.dtype == torch.bfloat16
-    nbad = int((a.view(torch.int16) != b.view(torch.int16)).sum().item())
-    assert nbad == 0, f"{nbad} outputs differ from the two-column kernel"
+    H, W = a.shape[-2:]
+    up = _up_rows(H).to(a.device)[:, None].expand(H, W)
+    sel = torch.ones((H, W), dtype=torch.bool, device=a.device) if mask is None else mask
+    fwd, rev = (sel & ~up).expand_as(a), (sel & up).expand_as(a)
+    nbad = int((a.view(torch.int16) != b.view(torch.int16))[fwd].sum().item())
+    assert nbad == 0, f"{nbad} outputs of downward bands differ from the two-column kernel"
+    if bool(rev.any()):
+        fa, fb = a[rev].float(), b[rev].float()
+        assert torch.equal(torch.isnan(fa), torch.isnan(fb))
+        fin = torch.isfinite(fb)
+        assert torch.equal(fa[~fin & ~torch.isnan(fb)], fb[~fin & ~torch.isnan(fb)])
+        d = (fa[fin] - fb[fin]).abs()
+        tol = 2.0 ** -7 * torch.maximum(fa[fin].abs(), fb[fin].abs()) + 1e-6
+        assert bool((d <= tol).all()), f"{int((d > tol).sum())} outputs of upward bands beyond one bf16 step"
 
 
 def test_layout():
@@ -69,7 +97,7 @@ def test_fused4_bit_identical_to_two_column_and_vs_oracle(shape, off, monkeypatc
     y4 = _run(x, conv, off, monkeypatch, False)
     y2 = _run(x, conv, off, monkeypatch, True)
     _same(y4, y2)
-    # What pins this kernel at the north_star's 1e-5 is the bit-identity above: the two-column
+    # What pins this kernel at the north_star's 1e-5 is the agreement above: the two-column
     # kernel is oracle-checked at 1e-5 in fp32 (tests/test_gpu_pipeline.py).  Against the fp64
     # oracle directly, each bf16 output is one rounding of an fp32 value within ~1e-6 of the
     # oracle's: per element |got - ref| <= 2^-8 |ref| (half an ulp is 2^-9 |ref| at most; the
@@ -104,16 +132,15 @@ def test_fused4_nonfinite_at_band_and_window_edges(off, monkeypatch):
         x[0, c, r, q] = vals[i % 3]
     y4 = _run(x, conv, off, monkeypatch, False)
     y2 = _run(x, conv, off, monkeypatch, True)
-    # every output farther than 3 rows / columns from a planted value is finite and bit-identical
-    # to the two-column kernel's; near one, a zero-weight tap of a window's column class may
+    # every output farther than 3 rows / columns from a planted value is finite and agrees with
+    # the two-column kernel's (_same); near one, a zero-weight tap of a window's column class may
     # carry the non-finite value differently (a 240-column window's class can differ from its
     # two 120-column windows': DESIGN.md section 3), but the value reaches the output near it
     near = torch.zeros((H, W), dtype=torch.bool)
     for _, r, q in pts:
         near[max(r - 3, 0):r + 4, max(q - 3, 0):q + 4] = True
     far = ~near.to(DEV)
-    a, b = y4[0][:, far], y2[0][:, far]
-    assert torch.isfinite(a.float()).all()
-    assert int((a.view(torch.int16) != b.view(torch.int16)).sum().item()) == 0
+    assert torch.isfinite(y4[0][:, far].float()).all()
+    _same(y4, y2, far)
     for _, r, q in pts:
         assert not torch.isfinite(y4[0, :, max(r - 3, 0):r + 4, max(q - 3, 0):q + 4].float()).all()

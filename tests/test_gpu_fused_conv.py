@@ -131,103 +131,12 @@ def test_fused_conv_nan_inf_positions_match_stream_kernel(dt, off):
     torch.testing.assert_close(y[fin], ref[fin], rtol=1e-5, atol=1e-5 * scale)
 
 
-# ---- the four-column HexConv2d kernel (fused4.hip, MD 1; round 5) ---------------------------
-# bf16 in and out, C = O = 3, groups 1, widths a multiple of 4 run on k_fused4<OP, 1> when
-# HYGRID_FCONV4=1 (opt-in: measured 1.7 % slower than the two-column kernel); it evaluates
-# the two-column kernel's products and sums per output in the same order (the packed 7-tap
-# stencil, taps in order), so its output is asserted BIT-IDENTICAL to k_fused MD 1
-# (HYGRID_FCONV4=0), which the fp32 tests above pin to the oracle at 1e-5.
-
-def _fconv4(on, fn, *args, **kw):
-    """fn with the four-column kernel on (HYGRID_FCONV4=1, opt-in) or off (the default)."""
-    old = os.environ.get("HYGRID_FCONV4")
-    os.environ["HYGRID_FCONV4"] = "1" if on else "0"
-    try:
-        out = fn(*args, **kw)
-        torch.cuda.synchronize()
-        return out
-    finally:
-        if old is None:
-            del os.environ["HYGRID_FCONV4"]
-        else:
-            os.environ["HYGRID_FCONV4"] = old
+# (Round 5's four-column HexConv2d kernel, k_fused4 MD 1, opt-in and measured 1.7 % slower
+# than k_fused MD 1, was removed in round 6: layout modes 7 and 8 are gone.)
 
 
-def _two_col(fn, *args, **kw):
-    return _fconv4(False, fn, *args, **kw)
-
-
-def _same_bits(a, b):
-    d = (a != b) & ~(torch.isnan(a) & torch.isnan(b))
-    n = int(d.sum().item())
-    if n:
-        idx = d.nonzero()[:4].tolist()
-        raise AssertionError(f"{n} outputs differ from the two-column kernel: "
-                             f"{[(i, float(a[tuple(i)]), float(b[tuple(i)])) for i in idx]}")
-
-
-def test_fconv4_layout():
+def test_removed_layout_modes_are_invalid():
     from HyGrid import _abi
-    rows, own, halo = _abi.fused_layout(8)
-    assert rows % 6 == 0 and own == 240 and halo == 8
-
-
-@pytest.mark.parametrize("shape", [(1, 7, 8), (2, 19, 12), (1, 37, 248), (2, 100, 500),
-                                   (1, 130, 964), (1, 44, 3840)])
-@pytest.mark.parametrize("off", [0, 1])
-@pytest.mark.parametrize("bias", [True, False])
-def test_fconv4_bit_identical_to_two_column(shape, off, bias):
-    B, h, w = shape
-    k, b = _weights(3, 3, h + 3 * w + off)
-    if not bias:
-        b = None
-    g = torch.Generator(device=DEV).manual_seed(h * 5 + w)
-    x = (torch.rand((B, 3, h, w), generator=g, device=DEV) * 4 - 2).to(torch.bfloat16)
-    y4 = _fconv4(True, ops.hexconv2d, x, k, b, off, 2, padding=1, out_dtype=torch.bfloat16)
-    y2 = _two_col(ops.hexconv2d, x, k, b, off, 2, padding=1, out_dtype=torch.bfloat16)
-    _same_bits(y4, y2)
-    if shape == (1, 37, 248):   # and one rounding of the fp64 oracle, per element
-        ref = O.hexconv2d(x.double().cpu().numpy(), k.cpu().double().numpy(),
-                          None if b is None else b.cpu().double().numpy(), off, 2, padding=1)
-        got = y4.double().cpu().numpy()
-        tol = 2.0 ** -8 * np.abs(ref) + 1e-5 * np.abs(ref).max()
-        assert (np.abs(got - ref) <= tol).all()
-
-
-def test_fconv4_4k_batch_bit_identical():
-    """The driver's unfused-chain launch shape (4K RGB bf16) on two images."""
-    k, b = _weights(3, 3, 3)
-    g = torch.Generator(device=DEV).manual_seed(2)
-    x = torch.rand((2, 3, 2160, 3840), generator=g, device=DEV, dtype=torch.bfloat16)
-    y4 = _fconv4(True, ops.hexconv2d, x, k, b, 0, 2, padding=1, out_dtype=torch.bfloat16)
-    y2 = _two_col(ops.hexconv2d, x, k, b, 0, 2, padding=1, out_dtype=torch.bfloat16)
-    _same_bits(y4, y2)
-
-
-@pytest.mark.parametrize("off", [0, 1])
-def test_fconv4_nan_inf_at_band_and_window_edges(off):
-    """Non-finite inputs on the raster border and on the four-column kernel's own window / band
-    edges (hg_fused_layout(8)): the padding is selected zeros, so every output whose taps read a
-    planted value is non-finite exactly as in the two-column kernel, and every other output is
-    bit-identical."""
-    from HyGrid import _abi
-    rows, own, _ = _abi.fused_layout(8)
-    B, h, w = 2, 2 * rows + 20, 2 * own + 12
-    k, b = _weights(3, 3, 29 + off)
-    g = torch.Generator(device=DEV).manual_seed(31)
-    x = torch.rand((B, 3, h, w), generator=g, device=DEV)
-    nan, inf = float("nan"), float("inf")
-    x[0, 0, 0, :] = nan
-    x[0, 1, h - 1, 5] = inf
-    x[0, 2, 11, 0] = -inf
-    x[1, 0, 17, w - 1] = nan
-    for c0 in (own - 1, own, 2 * own - 1, 2 * own):
-        x[1, 1, 5 + c0 % 7, c0] = nan
-    for r0 in (rows - 1, rows, 2 * rows - 1, 2 * rows):
-        x[1, 2, r0, 61 + r0 % 5] = inf
-    x = x.to(torch.bfloat16)
-    y4 = _fconv4(True, ops.hexconv2d, x, k, b, off, 2, padding=1, out_dtype=torch.bfloat16)
-    y2 = _two_col(ops.hexconv2d, x, k, b, off, 2, padding=1, out_dtype=torch.bfloat16)
-    assert torch.equal(torch.isnan(y4), torch.isnan(y2))
-    assert torch.equal(torch.isinf(y4), torch.isinf(y2))
-    _same_bits(y4, y2)
+    for md in (7, 8):
+        with pytest.raises(ValueError):
+            _abi.fused_layout(md)

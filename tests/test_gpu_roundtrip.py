@@ -105,68 +105,14 @@ def test_roundtrip_nonfinite_inputs_stay_local():
     torch.testing.assert_close(y[far].double(), ref[far], rtol=1e-5, atol=1e-5)
 
 
-def _rt(x, monkeypatch, two_col, out_dtype=None):
-    """The fused round trip on the four-column kernel (rt4.hip, opt-in: HYGRID_RT4=1, widths a
-    multiple of 4) or on the two-column k_fused MD 2 (the default)."""
-    if two_col:
-        monkeypatch.delenv("HYGRID_RT4", raising=False)
-    else:
-        monkeypatch.setenv("HYGRID_RT4", "1")
-    y = ops.pipeline_r2h_h2r(x, out_dtype=out_dtype)
-    torch.cuda.synchronize()
-    monkeypatch.delenv("HYGRID_RT4", raising=False)
-    assert y is not None
-    return y
-
-
-@pytest.mark.parametrize("dt,out", [(torch.float32, torch.float32), (torch.bfloat16, torch.bfloat16),
-                                    (torch.float16, torch.float16), (torch.bfloat16, torch.float32),
-                                    (torch.float16, torch.float32)])
-@pytest.mark.parametrize("shape", [(1, 1, 8, 12), (2, 3, 64, 132), (1, 2, 91, 248), (1, 1, 37, 500),
-                                   (3, 1, 200, 964), (1, 3, 44, 1920)])
-def test_roundtrip_four_column_bit_identical_to_two_column(shape, dt, out, monkeypatch):
-    """rt4.hip evaluates k_fused MD 2's products and sums per output column in the same order
-    (the packed vertical blend's halves are IEEE fmaf), so its output is bit-identical to the
-    two-column kernel's, which is oracle-checked at 1e-5 above; one shape per dtype pair is
-    also checked against the oracle directly."""
-    g = torch.Generator(device=DEV).manual_seed(sum(shape))
-    x = (torch.rand(shape, generator=g, device=DEV) * 4 - 2).to(dt)
-    y4 = _rt(x, monkeypatch, False, out)
-    y2 = _rt(x, monkeypatch, True, out)
-    assert y4.dtype == y2.dtype == out
-    # bit-identical up to the sign of an exact zero: where every r2h tap of a column lies
-    # outside the raster both kernels multiply zero weights by whatever their clamped loads
-    # hold there (different columns for 2- and 4-column lanes), so an output that is exactly
-    # 0 may be +0 in one and -0 in the other (the reference's masked gather gives +0)
-    diff = (y4 != y2) & ~(torch.isnan(y4) & torch.isnan(y2))
-    nbad = int(diff.sum().item())
-    if nbad:
-        idx = diff.nonzero()[:4].tolist()
-        det = [(i, float(y4[tuple(i)]), float(y2[tuple(i)])) for i in idx]
-        raise AssertionError(f"{nbad} outputs differ from the two-column kernel: {det}")
-    if shape == (1, 2, 91, 248):
-        ref = oracle_roundtrip(x.float().cpu())
-        ulp = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11, torch.float32: 1e-5}[out]
-        scale = np.abs(ref).max()
-        np.testing.assert_allclose(y4.double().cpu().numpy(), ref, rtol=ulp, atol=ulp * scale)
-
-
-def test_roundtrip_four_column_layout():
-    from HyGrid import _abi
-    rows, own, halo = _abi.fused_layout(7)
-    assert rows % 6 == 0 and own == 240 and halo == 8
-
-
-@pytest.mark.parametrize("md", [2, 7])
+@pytest.mark.parametrize("md", [2])
 def test_roundtrip_nonfinite_at_band_and_window_edges(md, monkeypatch):
-    """Band / window edges of the kernel that runs (md 2: the two-column k_fused MD 2, the
-    default; md 7: the four-column rt4.hip, HYGRID_RT4=1), from hg_fused_layout (not hard-coded):
+    """Band / window edges of the kernel that runs (md 2: k_fused MD 2; round 5's opt-in
+    four-column rt4.hip was removed in round 6), from hg_fused_layout (not hard-coded):
     non-finite inputs on the last row of a band and the first of the next, on the last owned
     column of a window and the first of the next; everything farther than 3 samples stays
     finite and matches the oracle, and every planted point reaches the output next to it."""
     from HyGrid import _abi
-    if md == 7:
-        monkeypatch.setenv("HYGRID_RT4", "1")
     rows, own, _ = _abi.fused_layout(md)
     H, W = 2 * rows + 10, 2 * own + 12
     g = torch.Generator().manual_seed(7)

@@ -18,7 +18,7 @@ slp=-fno-slp-vectorize; [ "${SLP:-0}" = 1 ] && slp=
     -I"$PKG/csrc" -c "$PKG/csrc/$SRC" -o "$OBJ/variants/${base}_$NAME.o"
 objs=()
 # FULL=1: every object of the library (for entry points outside the fused pipeline, e.g. the conv)
-list="abi pipeline fused fused4 rt4"
+list="abi pipeline fused fused4"
 [ "${FULL:-0}" = 1 ] && list=$(cd "$OBJ" && ls *.o | sed 's/\.o$//')
 for o in $list; do
     if [ "$o" = "$base" ]; then objs+=("$OBJ/variants/${base}_$NAME.o"); else objs+=("$OBJ/$o.o"); fi
