@@ -392,20 +392,13 @@ __device__ __forceinline__ void cd_wait_vm() {
     __builtin_amdgcn_s_waitcnt((0x0f70 & ~0xf) | (N & 0xf) | ((N >> 4) << 14));
 }
 
-// WDB: weight chunks double-buffered (the next chunk's DMA overlaps this chunk's MFMAs; 71 KB of
-// LDS -> 2 workgroups per CU) or single-buffered (the DMA of chunk i + 1 is issued once chunk i's
-// MFMAs are done and waited for at the top of the next chunk; 47 KB -> 3 workgroups per CU, whose
-// MFMAs cover each other's waits)
-// NQT: 16-column tiles per workgroup (4; 3 with PSB1 = one raw-P buffer is the 4-waves-per-SIMD
-// build: 48 accumulators and <= 40 KB of LDS, so four workgroups fit a CU; round 5)
-#ifndef CD_OPQ
-#define CD_OPQ 1                      // DMA address terms recomputed per chunk (see dma_w)
-#endif
-#ifndef CD_WPE3
-#define CD_WPE3 4                     // waves per SIMD asked of the allocator for the NQT 3 build
-#endif
-template <typename Tout, int NOT, bool WDB, int NQT = 4, bool PSB1 = false>
-__global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(NQT == 3 ? CD_WPE3 : 1)))
+// Weight chunks are single-buffered: the DMA of chunk i + 1 is issued once chunk i's MFMAs are
+// done and waited for at the top of the next chunk (47 KB of LDS -> 3 workgroups per CU, whose
+// MFMAs cover each other's waits; double-buffered, 71 KB and 2 workgroups per CU, was 18 %
+// slower, and 3 column tiles with one raw-P buffer for a 4th wave per SIMD 4 % slower: both
+// removed in round 6).  The raw P rows are double-buffered.
+template <typename Tout, int NOT>
+__global__ __launch_bounds__(CM_THREADS) __attribute__((amdgpu_waves_per_eu(1)))
 void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
                                                                    const cm_u4* __restrict__ wf,
                                                                    const int* __restrict__ flag,
@@ -419,8 +412,9 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
     constexpr int PPW = CM_CC * CM_PR / 4;                // raw P row pieces per wave (12)
     static_assert(WPC % 4 == 0, "pieces");
     // one LDS array (so the DMA's M0 bases come from it): [psb | wsb x 2 | praw x 2]
-    constexpr int LPSB = CB_PSZ * 16, LWSB = WSZ * 16, LPRAW = CD_PRAW * 4, NWB = WDB ? 2 : 1;
-    constexpr int NPB = PSB1 ? 1 : 2;                     // raw P buffers
+    constexpr int NQT = 4;                                // 16-column tiles per workgroup
+    constexpr int LPSB = CB_PSZ * 16, LWSB = WSZ * 16, LPRAW = CD_PRAW * 4, NWB = 1;
+    constexpr int NPB = 2;                                // raw P buffers
     constexpr int TQ = 16 * NQT;                          // output columns of this workgroup
     __shared__ __attribute__((aligned(16))) unsigned char lds[LPSB + NWB * LWSB + NPB * LPRAW];
     cm_u4* const psb = reinterpret_cast<cm_u4*>(lds);
@@ -471,14 +465,13 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
     const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
         (void*)wf, (short)0, 0x7fffffff, 0x00020000);
 
-    // CD_OPQ: the DMA address terms are recomputed at every chunk from values the compiler
-    // cannot see through (no hoisting: the hoisted per-piece offsets spilled 57-73 SGPRs)
+    // the DMA address terms are recomputed at every chunk from values the compiler cannot see
+    // through (no hoisting: the hoisted per-piece offsets spilled 57-73 SGPRs, round 5)
     auto opq = [](int v) {
-        if constexpr (CD_OPQ) asm volatile("" : "+s"(v));
+        asm volatile("" : "+s"(v));
         return v;
     };
-    auto dma_w = [&](int ci) {                            // chunk ci's weights -> buffer
-        const int buf = WDB ? (ci & 1) : 0;
+    auto dma_w = [&](int ci) {                            // chunk ci's weights -> the buffer
         const int wvo = opq(wv);
         // weights: pieces j = wv * WPW + i of the chunk's (pt, kb) blocks of CM_O * 4 fragments
 #pragma unroll
@@ -486,7 +479,7 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
             const int j = wvo * WPW + i;
             const int blk = j / (CM_O / 16), part = j % (CM_O / 16);   // (pt * 2 + kb), 1-KiB part
             const unsigned so = (unsigned)((((int64_t)ci * 6 + blk) * Opad + o0) * 64 + part * 1024);
-            const unsigned lda = lds0 + LPSB + buf * LWSB + (blk * CM_O * 4) * 16 + part * 1024;
+            const unsigned lda = lds0 + LPSB + (blk * CM_O * 4) * 16 + part * 1024;
             const unsigned vo = lane * 16u;
             unsigned keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
@@ -495,7 +488,7 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
         }
     };
     auto dma_p = [&](int ci) {                            // chunk ci's raw P rows -> buffer (ci & 1)
-        const int buf = PSB1 ? 0 : ci & 1;
+        const int buf = ci & 1;
         if (interior) {
             const int wvo = opq(wv), ho = opq(G.h), wo = opq(G.w);
             // P rows: pieces j = wv * PPW + i = (cc, pr); lanes 0-39 one dword each
@@ -519,28 +512,19 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
         }
     };
     // every wave issues the same number of DMA instructions per chunk (counted waits)
-    constexpr int NW = WPW, NP_ = PPW;
+    constexpr int NP_ = PPW;
 
     dma_w(0);
     dma_p(0);
     for (int ci = 0; ci < nch; ++ci) {
-        const int buf = PSB1 ? 0 : ci & 1;
+        const int buf = ci & 1;
         const int c0 = ci * CM_CC;
         // chunk ci's pieces are done once at most the ones issued after them are outstanding
-        // (vmcnt counts them in issue order): double-buffered, W(ci+1) and P(ci+1); single,
-        // only P(ci+1) (W(ci) was issued at the end of chunk ci-1, before P(ci+1)).  PSB1: P(ci+1)
-        // is issued after this chunk's repack (one raw buffer), so everything issued is waited for
-        if (PSB1) {
-            cd_wait_vm<0>();
-        } else if (ci + 1 < nch) {
-            if constexpr (WDB) {
-                dma_w(ci + 1);
-                dma_p(ci + 1);
-                if (interior) cd_wait_vm<NW + NP_>(); else cd_wait_vm<NW>();
-            } else {
-                dma_p(ci + 1);
-                if (interior) cd_wait_vm<NP_>(); else cd_wait_vm<0>();
-            }
+        // (vmcnt counts them in issue order): only P(ci+1) (W(ci) was issued at the end of
+        // chunk ci-1, before P(ci+1))
+        if (ci + 1 < nch) {
+            dma_p(ci + 1);
+            if (interior) cd_wait_vm<NP_>(); else cd_wait_vm<0>();
         } else {
             cd_wait_vm<0>();
         }
@@ -556,11 +540,6 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
                 psb[f] = cm_u4{v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
                                v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16)};
             }
-        }
-        if (PSB1 && interior && ci + 1 < nch) {
-            __builtin_amdgcn_s_waitcnt(0xc07f);           // this wave's repack reads are done
-            __builtin_amdgcn_s_barrier();                 // ... and every wave's: the raw buffer is free
-            dma_p(ci + 1);
         }
         if (!interior && tid < 3 * CB_PP) {               // the register staging (padding rules)
             const int pc = tid % CB_PP, ph = tid / CB_PP;
@@ -590,7 +569,7 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
         __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0): this wave's LDS writes
         __builtin_amdgcn_s_barrier();                     // psb and the weights complete
         // ---- 2 k blocks x NQT column tiles x 3 weight parts x NOT channel tiles -----------
-        const cm_u4* const wsb = reinterpret_cast<const cm_u4*>(lds + LPSB + (WDB ? (ci & 1) : 0) * LWSB);
+        const cm_u4* const wsb = reinterpret_cast<const cm_u4*>(lds + LPSB);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             cm_b8 bf[NQT];
@@ -611,9 +590,7 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_s_barrier();                     // psb / this buffer free again
-        if constexpr (!WDB) {
-            if (ci + 1 < nch) dma_w(ci + 1);              // the single weight buffer is free
-        }
+        if (ci + 1 < nch) dma_w(ci + 1);                  // the single weight buffer is free
     }
 
     if (r >= G.ho) return;
@@ -692,28 +669,10 @@ int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_
             cm_u4* wfr = static_cast<cm_u4*>(ws);
             int* flg = reinterpret_cast<int*>(static_cast<char*>(ws) + wbytes);
             hipLaunchKernelGGL(k_wsplit_bf16, dim3(nch, Opad / 16), dim3(128), 0, st, k, wfr, flg, G.C, G.O, Opad);
-            // weight chunks single-buffered (A/B switch HYGRID_CONV_WDB=1: double-buffered)
-            const bool wdb = env_is("HYGRID_CONV_WDB", "1");
-            // HYGRID_CONV_NQT=3: 3 column tiles per workgroup and one raw-P buffer (4 waves/SIMD)
-            if (nt == 4 && !wdb && env_is("HYGRID_CONV_NQT", "3")) {
-                G.ntq = (G.wo + 48 - 1) / 48;
-                const int64_t blocks3 = B * (int64_t)G.ntq * G.ntr * G.nto;
-                if (blocks3 > INT_MAX) { (void)hipFreeAsync(ws, st); return HG_EUNSUP; }
-                if (y_dtype == HG_BF16)
-                    hipLaunchKernelGGL((k_hexconv_mfma_bf16d<__bf16, 4, false, 3, true>), dim3((unsigned)blocks3), blk, 0, st,
-                                       (const __bf16*)x, wfr, flg, b, (__bf16*)y, G, Opad);
-                else
-                    hipLaunchKernelGGL((k_hexconv_mfma_bf16d<float, 4, false, 3, true>), dim3((unsigned)blocks3), blk, 0, st,
-                                       (const __bf16*)x, wfr, flg, b, (float*)y, G, Opad);
-                const int ls3 = launch_status();
-                const hipError_t fe3 = hipFreeAsync(ws, st);
-                return ls3 != HG_OK ? ls3 : (int)fe3;
-            }
-#define HG_CD_LAUNCH2(TO, NT_, WDB_)                                                          \
-            hipLaunchKernelGGL((k_hexconv_mfma_bf16d<TO, NT_, WDB_>), grid, blk, 0, st, (const __bf16*)x, wfr, flg, b, (TO*)y, G, Opad);
+#define HG_CD_LAUNCH2(TO, NT_)                                                                \
+            hipLaunchKernelGGL((k_hexconv_mfma_bf16d<TO, NT_>), grid, blk, 0, st, (const __bf16*)x, wfr, flg, b, (TO*)y, G, Opad);
 #define HG_CD_LAUNCH(TO)                                                                      \
-            if (nt == 2) { if (wdb) { HG_CD_LAUNCH2(TO, 2, true) } else { HG_CD_LAUNCH2(TO, 2, false) } } \
-            else { if (wdb) { HG_CD_LAUNCH2(TO, 4, true) } else { HG_CD_LAUNCH2(TO, 4, false) } }
+            if (nt == 2) { HG_CD_LAUNCH2(TO, 2) } else { HG_CD_LAUNCH2(TO, 4) }
             if (y_dtype == HG_BF16) { HG_CD_LAUNCH(__bf16) } else { HG_CD_LAUNCH(float) }
 #undef HG_CD_LAUNCH
 #undef HG_CD_LAUNCH2

@@ -267,14 +267,11 @@ def test_mfma_bf16_dma_bit_identical_to_register_staging(case, pad, off):
 
 
 @pytest.mark.parametrize("case", DMA_CASES)
-@pytest.mark.parametrize("env", [("HYGRID_CONV_WDB", "1"), ("HYGRID_CONV_NT", "2"),
-                                 ("HYGRID_CONV_NQT", "3")])
+@pytest.mark.parametrize("env", [("HYGRID_CONV_NT", "2")])
 def test_mfma_bf16_dma_weight_buffering_and_tiles_bit_identical(case, env):
-    """The single-buffered weight chunks (default) and the double-buffered ones
-    (HYGRID_CONV_WDB=1) stage the same fragments for the same MFMAs: bit-identical outputs; two
-    output-channel tiles per workgroup (HYGRID_CONV_NT=2) compute each output's sum in the same
-    order: bit-identical too; so do three 16-column tiles per workgroup with one raw-P buffer
-    (HYGRID_CONV_NQT=3, the 4-waves-per-SIMD build)."""
+    """Two output-channel tiles per workgroup (HYGRID_CONV_NT=2) compute each output's sum in
+    the same order as four: bit-identical outputs.  (Round 5's double-buffered weight chunks and
+    3-column-tile build, both slower, were removed in round 6.)"""
     B, C, O_, h, w = case
     k, b = _weights(O_, C, h * 3 + w)
     x = _bf16_input((B, C, h, w), h + 2 * w)

@@ -109,5 +109,7 @@ def test_rccl_world1_config3_shard(nccl_world1):
                     conv.bias.detach().cpu().double().numpy(), 0, 2, padding=1)
     ref = O.hex_to_rect(c, (2160, 3840), 1).reshape(3, 2160, 3840)
     got = y[127].double().cpu().numpy()
-    assert np.abs(got - ref).max() <= 2.0 ** -8 * np.abs(ref).max()
+    # per element: one bf16 rounding of |ref| plus an absolute floor of 1e-5 max|ref|
+    tol = 2.0 ** -8 * np.abs(ref) + 1e-5 * np.abs(ref).max()
+    assert not (np.abs(got - ref) > tol).any(), int((np.abs(got - ref) > tol).sum())
     del x, y
