@@ -45,11 +45,6 @@ namespace hg {
 #ifndef F4_REV
 #define F4_REV 1                       // odd full bands walk upwards (shared halo rows in L2, below)
 #endif
-#ifndef F4_NOMEM
-#define F4_NOMEM 0                     // diagnostic floor: every row load / store hits row 0 of its
-                                       // plane (cache-resident), the arithmetic unchanged (1: loads
-                                       // and stores, 2: loads only, 3: stores only)
-#endif
 constexpr int F4_GW = 4, F4_THREADS = 256;
 constexpr int F4_HL = 8, F4_OWN = 240;  // window halo (left) and owned columns
 constexpr int F4_RB = F4_RB_;
@@ -133,7 +128,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     }
 
     // ---- per-lane column weights of the two pairs (geometry_np.py:441-449, 514-517) -------
-    // with the h2r 0.75 folded in (u' = 0.75 u: FU_FOLD of k_fused)
+    // with the h2r 0.75 folded in (u' = 0.75 u, as k_fused MD 0)
     float we[2][3], wo[2][3];
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -178,7 +173,6 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
     const unsigned xplane = (unsigned)(cstride * 2), yplane = (unsigned)(ostride * 2);
     const unsigned xrow = (unsigned)F.w * 2u, yrow = (unsigned)F.w2 * 2u;
     auto row_off = [&](int r) -> unsigned {
-        if (F4_NOMEM == 1 || F4_NOMEM == 2) return 0u;
         return (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)min(max(r, 0), F.h - 1) * xrow));
     };
 
@@ -259,7 +253,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             fu_sfor<0, C>([&](auto Cc) {
                 constexpr int c = decltype(Cc)::value;
                 float ue[2], uo[2];
-                // vertical blend, packed (k_fused FU_VPK), for both pairs: a x[r-1] + b x[r] + c x[r+1]
+                // vertical blend, packed (as k_fused), for both pairs: a x[r-1] + b x[r] + c x[r+1]
                 auto vblend = [&](const fu_f2 (&X)[3][C]) {
                     if constexpr (RC == 1) return fu_pfma<1, false>(Lxy, X[S1][c], fu_pmul<0>(Lxy, X[XM][c]));
                     else if constexpr (RC == 2) return fu_pfma<0, false>(Lzw, X[XQ][c], fu_pmul<1>(Lxy, X[S1][c]));
@@ -335,7 +329,7 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             constexpr int PH = decltype(PHc)::value;
             constexpr int S0 = PH % 3;
             constexpr int PAR = UP ? (PH + 1) & 1 : PH & 1;
-            const unsigned so = (F4_NOMEM == 1 || F4_NOMEM == 3) ? 0u : (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)row(k) * yrow));
+            const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((int)((unsigned)row(k) * yrow));
 #pragma unroll
             for (int o = 0; o < O; ++o) {
                 const fu_f2 zA = ZA[S0][o], zB = ZB[S0][o];

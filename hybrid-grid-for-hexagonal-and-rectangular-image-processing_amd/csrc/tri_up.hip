@@ -70,9 +70,6 @@ namespace hg {
 #ifndef TU_CPP
 #define TU_CPP 24           // planes per unit when the grid has a wave per unit (round 5)
 #endif
-#ifndef TU_DIAG
-#define TU_DIAG 0           // diagnostics (A/B variants only): 1 = no stores, 2 = no row loads, 3 = neither
-#endif
 constexpr int TU_THREADS = 256;
 #ifndef TU_KDIV
 #define TU_KDIV 1           // output columns per lane = the natural K / TU_KDIV (A/B variants)
@@ -191,14 +188,6 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
             yo[k] = (unsigned)a * orow;
 #pragma unroll
             for (int kk = 0; kk < K; ++kk) {
-                if constexpr ((TU_DIAG & 4) != 0) {   // (diag: one record per unit, timing only)
-                    if (k > 0 || kk > 0) {
-                        for (int v = 0; v < NV; ++v) off[k][kk][v] = off[0][0][v] + kk * E;
-                        if constexpr (!NEAR)
-                            for (int v = 0; v < 3; ++v) wt[k][kk][v] = wt[0][0][v];
-                        continue;
-                    }
-                }
                 // one sample's fp64 temporaries at a time (the scheduler would otherwise
                 // interleave the samples and spill)
                 __builtin_amdgcn_sched_barrier(0);
@@ -244,7 +233,7 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
                 const unsigned so = po + (unsigned)min(rlo + q, D.h - 1) * rowb;
                 auto* const l0 = (__attribute__((address_space(3))) void*)(ring + SL * TU_SLOT_ + q * TU_ROWB);
                 auto* const l1 = (__attribute__((address_space(3))) void*)(ring + SL * TU_SLOT_ + q * TU_ROWB + 256);
-                const unsigned so_ = TU_DIAG >= 2 ? 0x80000000u : so;   // (diag: out of range)
+                const unsigned so_ = so;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, l0, 4, voff0, so_, 0, 0);
                 if (lane < 8) __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, l1, 4, voff1, so_, 0, 0);
             }
@@ -268,7 +257,7 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
             const unsigned po = pi < np ? (unsigned)pi * planeb : (unsigned)np * planeb;
 #pragma unroll
             for (int q = 0; q < TU_NR_; ++q) {
-                const unsigned so = TU_DIAG >= 2 ? 0x80000000u : po + (unsigned)min(rlo + q, D.h - 1) * rowb;
+                const unsigned so = po + (unsigned)min(rlo + q, D.h - 1) * rowb;
                 rv[SL][q][0] = __builtin_amdgcn_raw_buffer_load_b32(xr, voff0, so, 0);
                 rv[SL][q][1] = __builtin_amdgcn_raw_buffer_load_b32(xr, voff1v, so, 0);
             }
@@ -313,7 +302,7 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
                     if constexpr (SB == 32) pk[kk] = bits;
                     else pk[(kk * SB) / 32] |= bits << ((kk * SB) % 32);
                 }
-                tu_store<OB>(pk, yr, (TU_DIAG & 1) ? 0x80000000u : vo, __builtin_amdgcn_readfirstlane(so + yo[k]));
+                tu_store<OB>(pk, yr, vo, __builtin_amdgcn_readfirstlane(so + yo[k]));
             }
         };
         if constexpr (TU_VLD) {
@@ -359,7 +348,7 @@ void k_tri_up(const Tin* __restrict__ x, Tout* __restrict__ y, TriUpGeom D) {
                     if constexpr (SB == 32) pk[kk] = bits;
                     else pk[(kk * SB) / 32] |= bits << ((kk * SB) % 32);
                 }
-                tu_store<OB>(pk, yr, (TU_DIAG & 1) ? 0x80000000u : vo, __builtin_amdgcn_readfirstlane(so + yo[k]));
+                tu_store<OB>(pk, yr, vo, __builtin_amdgcn_readfirstlane(so + yo[k]));
             }
         };
         tu_static_for<TU_PDP_>([&](auto Pc) { dma(decltype(Pc)::value, Pc); });   // prologue
