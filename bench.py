@@ -15,7 +15,7 @@ GPU yet; never an exec) and exits with its return code; under a launcher, WORLD_
 equal --gpus or the bench exits with status 2.  value = all ranks' input pixels / the
 max-over-ranks wall time of K steps.  Every timed step, at every N including N = 1 (a
 world-1 process group), ends with per-image, per-channel sums of a row sample of its output
-(every 64th row) all-gathered over RCCL (the collective stays inside the timed
+(every 256th row) all-gathered over RCCL (the collective stays inside the timed
 loop; a few KB per rank), so the per-step work is the same at every N.  After the timed
 region, full per-image checksums are all-gathered, and (N>1) the full-output gather to
 rank 0 is timed and reported on its own (`gather`), never folded into `value`.
@@ -351,7 +351,7 @@ def main():
     else:
         from HyGrid import ops
         from HyGrid.HexFrames import HexConv2d
-        from HyGrid.pipeline import rect_hex_conv_rect, rect_hex_rect
+        from HyGrid.pipeline import hex_pyramid, rect_hex_conv_rect, rect_hex_rect
 
         gen = torch.Generator(device=dev).manual_seed(2 + rank)
         x = torch.rand((B, C, H, W), generator=gen, device=dev, dtype=bf16)
@@ -389,10 +389,13 @@ def main():
     sums_buf = {}
 
     def step_sums(y):
-        """Per-image, per-channel sums of every 64th output row, all-gathered over RCCL: the
+        """Per-image, per-channel sums of every 256th output row, all-gathered over RCCL: the
         collective every timed step ends with (a few KB per rank), at every N (N = 1: the
-        world-1 group).  One strided reduction kernel accumulating in fp32."""
-        s_ = torch.sum(y[:, :, ::64], (2, 3), dtype=torch.float32).to(cdev)
+        world-1 group).  Row sums first (contiguous inner reduction), then over the sampled
+        rows: every 64th row cost 0.037 ms per 4K b128 step this way, against 0.159 ms for one
+        reduction over both dims of the strided view (profiles/r06/step_sums_probe.txt); every
+        256th row (9 of 2160) keeps it near 0.01 ms.  The world-1 all-gather is 0.017 ms."""
+        s_ = torch.sum(y[:, :, ::256], -1, dtype=torch.float32).sum(-1).to(cdev)
         key = tuple(s_.shape)
         if key not in sums_buf:
             sums_buf[key] = torch.empty((world * s_.shape[0],) + key[1:], dtype=s_.dtype,
@@ -544,9 +547,24 @@ def main():
             return hx
 
         def run_pyramid(record, ev):
-            """HyGrid.pipeline.hex_pyramid's fused path: one hg_hex_pyramid_level pass per
-            level, level 0 straight from the rect image (rect -> hex made on the fly,
-            k_pyr_stream FR); HIP events per kernel."""
+            """HyGrid.pipeline.hex_pyramid, the product entry: the fused levels (level 0 straight
+            from the rect image) with the batch in two runs of images on two HIP streams, so
+            one run's launches fill the chip while the other's ramp up and drain (round 6);
+            HIP events on the caller's stream around the whole step."""
+            if record:
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                e[0].record()
+            outs = hex_pyramid(xp, gconv, levels=3, out_dtype=f16)
+            if record:
+                e[1].record()
+                ev.append(e)
+            if not levels:
+                levels.append(tuple(outs[-1].shape))
+            return outs[-1]
+
+        def run_pyramid_levels(record, ev):
+            """The same levels as one launch each on one stream (hg_hex_pyramid_level x 3):
+            HIP events per kernel, for the per-level breakdown."""
             if record:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 e[0].record()
@@ -567,7 +585,8 @@ def main():
             return cur
 
         steps_p = max(2, args.steps // 2)
-        _, el_p, sms_p = measure_line(run_pyramid, steps_p)
+        _, el_p, _ = measure_line(run_pyramid, steps_p)
+        _, el_p1, sms_p = measure_line(run_pyramid_levels, steps_p)
         _, el_pu, sms_pu = measure_line(run_pyramid_unfused, steps_p)
         lvl_bytes = []                                  # each level: read input + write output
         h_, w_ = Hp, Wp
@@ -590,8 +609,13 @@ def main():
         own_u = [Bp * C * 2 * v for v in own_u]
         pyramid = {"workload": "config5: 8K RGB fp16, r2h -> 3 x [depthwise Gaussian HexConv2d "
                                "-> hexresize /2]",
-                   "path": "hg_hex_pyramid_level x 3 (conv + hexresize, fp32 on chip; level 0 "
-                           "reads the rect image: rect -> hex made on the fly)",
+                   "path": "HyGrid.pipeline.hex_pyramid: hg_hex_pyramid_level x 3 (conv + "
+                           "hexresize, fp32 on chip; level 0 reads the rect image: rect -> hex "
+                           "made on the fly), the batch as 2 runs of images on 2 HIP streams",
+                   "one_stream": {"ms_per_step": round(el_p1 / steps_p * 1e3, 4),
+                                  "frac_of_peak": round(sum(lvl_bytes) / (el_p1 / steps_p) / PEAK_BPS, 4),
+                                  "what": "one launch per level on one stream (the kernels "
+                                          "below are timed this way)"},
                    "batch_per_gpu": Bp, "value": round(world * Bp * Hp * Wp * steps_p / el_p / 1e6, 1),
                    "unit": "Mpix/s", "ms_per_step": round(el_p / steps_p * 1e3, 4),
                    "dtype": "f16", "out_shape": list(levels[0]),

@@ -496,14 +496,15 @@ def pipeline_r2h_conv_h2r(x, kernel, bias, hex_size=None, rect_size=None, paddin
 
 
 def hex_pyramid_level(x, taps, bias=None, size=None, even_odd_offset=0, from_rect=False,
-                      out_dtype=None):
+                      out_dtype=None, out=None):
     """One hex Gaussian pyramid level in one pass: hexresize(HexConv2d_depthwise(x))
     (geometry_np.py:520-681 after HexFrames.py:96-169, radius 2, padding 1, pad value 0),
     with rect_to_hex(x) (geometry_np.py:358-519) first when from_rect.
 
     x: (B, C, h, w) device tensor; taps: the depthwise kernel (C, 1, 1, 7) or (C, 7);
-    size: (h1, w1), default (h // 2, w // 2).  Returns None when the fused kernel does
-    not cover the geometry / dtypes (the caller then runs the operators).
+    size: (h1, w1), default (h // 2, w // 2).  out: an optional contiguous (B, C, h1, w1)
+    tensor of out_dtype to write into (e.g. a slice of a larger batch).  Returns None when the
+    fused kernel does not cover the geometry / dtypes (the caller then runs the operators).
     """
     _abi.require_device(x)
     while x.dim() < 4:
@@ -515,7 +516,14 @@ def hex_pyramid_level(x, taps, bias=None, size=None, even_odd_offset=0, from_rec
     b = bias.detach().float().contiguous() if bias is not None else None
     if out_dtype is None:
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
-    y = torch.empty((B, C, h1, w1), dtype=out_dtype, device=x.device)
+    if out is None:
+        y = torch.empty((B, C, h1, w1), dtype=out_dtype, device=x.device)
+    else:
+        if (tuple(out.shape) != (B, C, h1, w1) or out.dtype != out_dtype
+                or out.device != x.device or not out.is_contiguous()):
+            raise ValueError(f"hex_pyramid_level: out must be a contiguous {(B, C, h1, w1)} "
+                             f"{out_dtype} tensor on {x.device}")
+        y = out
     st = _abi.lib().hg_hex_pyramid_level(
         _abi.ptr(x), _abi.ptr(y), _abi.dtype_code(x.dtype), _abi.dtype_code(out_dtype), B, C,
         h, w, h1, w1, _abi.ptr(k), _abi.ptr(b), int(even_odd_offset), int(bool(from_rect)),

@@ -223,11 +223,13 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
         fu_f2 XA[3][C], XB[3][C];           // rect rows as f32 pairs A / B, slot k % 3
         fu_f2 ZA[3][O], ZB[3][O];           // conv rows being accumulated, slot k % 3
 
-        auto issue = [&](auto SLc, int r) {
+        // live false: the loads return zeros without a memory access (an offset past the buffer)
+        auto issue = [&](auto SLc, int r, bool live = true) {
             constexpr int SL = decltype(SLc)::value;
             const unsigned so = row_off(r);
+            const unsigned vo = live ? xoff : 0x80000000u;
 #pragma unroll
-            for (int c = 0; c < C; ++c) raw[SL][c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, xoff, so + c * xplane, 0);
+            for (int c = 0; c < C; ++c) raw[SL][c] = __builtin_amdgcn_raw_buffer_load_b64(xrs, vo, so + c * xplane, 0);
         };
         auto convert = [&](auto RSc, auto XSc) {
             constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
@@ -389,9 +391,9 @@ void k_fused4(const __bf16* __restrict__ x, const float* __restrict__ kern,
             constexpr int PH = decltype(PHc)::value;
             __builtin_amdgcn_sched_barrier(0);
             convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row row(k+2)
-            // (past the band's last halo row the load repeats that row: an L2 hit, not a
-            // 31st row from HBM)
-            issue(IC<(PH + 2 + PD) % 6>{}, row(min(k + 2 + PD, n + 1)));
+            // (a row past the band's last halo row is never read: its load goes out of range,
+            // no memory access, instead of a 31st row from HBM)
+            issue(IC<(PH + 2 + PD) % 6>{}, row(min(k + 2 + PD, n + 1)), k + 2 + PD <= n + 1);
             const float4 L = lnext;
             lnext = lut[min(max(lut_e(k + 2), 0), NLUT - 1)];
             urow(PHc, L, std::true_type{}, std::true_type{});           // u row row(k+1)

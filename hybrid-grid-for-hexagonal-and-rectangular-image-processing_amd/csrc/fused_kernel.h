@@ -43,7 +43,9 @@ constexpr int FU_OWN = FU_OWN_;       // owned columns per 128-column window
 #define FU_RB_PYRS_ 24                // MD 5 (= MD 4 on short bands for small levels)
 #endif
 #ifndef FU_RB_RT_
-#define FU_RB_RT_ 30                  // MD 2: rows per band (66 -> 30: 0.321 -> 0.307 ms, r03 A/B)
+#define FU_RB_RT_ 12                  // MD 2: rows per band (66 -> 30: 0.321 -> 0.307 ms, r03 A/B;
+                                      // 30 -> 12 with the upward bands of round 6: -2.3 %, which
+                                      // also shortens the launch's tail, profiles/r06/)
 #endif
 constexpr int FU_RB = FU_RB_;
 constexpr int FU_RB_CONV = FU_RB_CONV_;
@@ -518,11 +520,13 @@ void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
         float ZE[3][O], ZO[3][O];           // MD 2: u rows (= its conv rows), slot k % 3
         fu_f2 ZP[3][O];                     // conv rows being accumulated, (even, odd) pairs
 
-        auto issue = [&](auto SLc, int r) {
+        // live false: the loads return zeros without a memory access (an offset past the buffer)
+        auto issue = [&](auto SLc, int r, bool live = true) {
             constexpr int SL = decltype(SLc)::value;
             const unsigned so = row_off(r);
+            const unsigned vo = live ? xoff : 0x80000000u;
     #pragma unroll
-            for (int c = 0; c < C; ++c) raw[SL][c] = fu_load<Tin>(xrs, xoff, so + c * xplane);
+            for (int c = 0; c < C; ++c) raw[SL][c] = fu_load<Tin>(xrs, vo, so + c * xplane);
         };
         auto convert = [&](auto RSc, auto XSc) {
             constexpr int RS = decltype(RSc)::value, XS = decltype(XSc)::value;
@@ -817,9 +821,10 @@ void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
             // scheduler otherwise hoists loads many steps ahead (266 VGPRs, 1 wave / SIMD)
             __builtin_amdgcn_sched_barrier(0);
             convert(IC<(PH + 2) % 6>{}, IC<(PH + 2) % 3>{});            // rect row row(k+2)
-            // past the band's last halo row (row(n+1)) the load repeats that row: an L2 hit
-            // instead of PD rows per band from HBM that nothing reads (round 6)
-            issue(IC<(PH + 2 + PD) % 6>{}, row(min(k + 2 + PD, n + 1)));
+            // rows past the band's last halo row (row(n+1)) are never read: their loads go out
+            // of range (no memory access) instead of fetching PD rows per band from HBM
+            // (round 6; repeating row(n+1) instead, an L2 hit, measured slower)
+            issue(IC<(PH + 2 + PD) % 6>{}, row(min(k + 2 + PD, n + 1)), k + 2 + PD <= n + 1);
             const float4 L = lnext;
             lnext = lut[min(max(lut_e(k + 2), 0), NLUT - 1)];
             urow(PHc, L, std::true_type{}, std::true_type{});           // u row row(k+1)

@@ -321,7 +321,9 @@ static int hd_launch(const void* src, void* dst, HexDownGeom& D, hipStream_t st)
     // Round 5: one wave per unit and ~HD_CPP planes per unit (the records amortised over more
     // planes; fewer, longer-lived units contend less): 4K -> 2K bf16 b32 0.496 -> 0.429 ms, 8K ->
     // 4K fp16 b8 -1.9 % (profiles/r05/hexresize_grid_ab.txt).  HYGRID_TSK_GRID=0: the old rule.
-    const bool grid = !env_is("HYGRID_TSK_GRID", "0");
+    // (only with >= 2 chunks of planes: below that the old rule's plane chunks fill the
+    // resident waves, e.g. a single RGB image's 3 planes, as k_tri_up does)
+    const bool grid = !env_is("HYGRID_TSK_GRID", "0") && D.planes >= 2 * HD_CPP;
     if (grid) nchunk = std::max<int64_t>(1, D.planes / HD_CPP);
     if (const char* e = getenv("HYGRID_TSK_CHUNKS"))   // A/B switch: plane chunks per tile
         nchunk = std::max<int64_t>(1, std::min<int64_t>(D.planes, atoi(e)));
@@ -364,7 +366,7 @@ int tristream_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t 
     // 128-column windows (4-B pieces) when upsampling or the rows are not 16-B aligned; a
     // lane owns K output columns of its window in groups of P adjacent ones (K = 4, or
     // fewer for narrow windows)
-    const double ratio = w1 > 1 ? (double)(w - 1) / (double)(w1 - 1) : 1.0;
+    const double ratio = (double)(w - 1) / (double)(w1 - 1);   // (tri_fast_ok: w1 > 1)
     const int DB = (ratio >= 0.75 && a16) ? 16 : 4, wc = 32 * DB + 16, al = DB / 2;
     const int P = DB == 16 ? HD_P16 : HD_P4;
     if (P == 2 && w1 < 2) return HG_EUNSUP;

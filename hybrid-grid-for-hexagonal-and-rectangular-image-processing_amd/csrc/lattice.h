@@ -194,6 +194,8 @@ __host__ __device__ __forceinline__ double axis_at_step(const Axis& a, int64_t k
 
 // tri_sample bit for bit, cheaper (32-bit lattice indices, no speculated division) when
 // tri_fast_ok(g) holds (host-checked by the streaming kernels that compute per-sample records).
+// (Both axes need n > 1: h1 == 1 or w1 == 1 calls -- one output row or column -- run on the
+// general kernels, which evaluate axis_at's n == 1 case; the streaming callers rely on it.)
 inline bool tri_fast_ok(const Geom& g) {
     const int64_t lim = (int64_t)1 << 22;   // |i_|, |j_| < 2^23 << 2^24
     return g.xs.n > 1 && g.ys.n > 1 && g.xs.step != 0.0 && g.ys.step != 0.0 && g.h < lim &&

@@ -430,8 +430,8 @@ int triup_try(int op, const void* src, void* dst, int sdt, int ddt, int64_t plan
     const Geom g = make_tri(h, w, h1, w1, op == HG_OP_HEXRESIZE ? 0.5 : 0.75);
     if (!tri_fast_ok(g)) return HG_EUNSUP;
     // upsampling only: output steps of at most one input sample in both directions
-    if ((double)(h - 1) > (double)(h1 - 1) || (w1 > 1 && (double)(w - 1) > (double)(w1 - 1)))
-        return HG_EUNSUP;
+    // (tri_fast_ok above: h1, w1 > 1)
+    if ((double)(h - 1) > (double)(h1 - 1) || (double)(w - 1) > (double)(w1 - 1)) return HG_EUNSUP;
     TriUpGeom D = {};
     double qmax;
     if (!tsk_rows_ok(g, &D.qmin, &qmax)) return HG_EUNSUP;

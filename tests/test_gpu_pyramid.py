@@ -197,6 +197,25 @@ def test_hex_pyramid_8k_batch8_first_last(monkeypatch):
             assert torch.equal(a[0], b[i])
 
 
+@pytest.mark.parametrize("B,groups", [(8, None), (8, 3), (5, 2), (3, 3)])
+def test_hex_pyramid_image_groups_on_streams_bit_identical(B, groups, monkeypatch):
+    """hex_pyramid's fused levels with the batch split into runs of images on separate HIP
+    streams (round 6; default 2 runs) write the same bits as one launch per level over the
+    whole batch: the work per image is the same kernel code, only the launches differ.  The
+    bench's 8 x 8K shape and uneven splits."""
+    conv = gaussian_conv()
+    gen = torch.Generator(device=DEV).manual_seed(10 + B)
+    H, W = (4320, 7680) if B == 8 else (272, 480)
+    x = torch.rand((B, 3, H, W), generator=gen, device=DEV, dtype=torch.float16)
+    ref = fused_levels_only(x, conv, monkeypatch)
+    with torch.no_grad():
+        got = hex_pyramid(x, conv, levels=3, groups=groups)
+        one = hex_pyramid(x, conv, levels=3, groups=1)
+    torch.cuda.synchronize()
+    for a, b, c in zip(got, ref, one):
+        assert a.shape == b.shape and torch.equal(a, b) and torch.equal(c, b)
+
+
 @pytest.mark.parametrize("H,W", [(540, 960), (136, 250)])
 def test_hex_pyramid_entry_matches_chain(H, W):
     """HyGrid.pipeline.hex_pyramid (the bench's config-5 step) gives the operator chain's
