@@ -70,62 +70,7 @@ def pyramid_fusable(conv):
             and conv.kernel.dtype == torch.float32)
 
 
-_STREAMS = {}
-
-
-def _side_streams(dev, n):
-    """n HIP streams of device dev, created once per process (a pool, not per call)."""
-    key = (dev.index, n)
-    if key not in _STREAMS:
-        _STREAMS[key] = [torch.cuda.Stream(dev) for _ in range(n)]
-    return _STREAMS[key]
-
-
-def _pyramid_fused_groups(x, conv, levels, out_dtype, l0_from_rect, groups):
-    """The fused levels with the batch split into `groups` runs of images, each run's level
-    chain on its own HIP stream (images are independent, every reference entry point is
-    per-image): one run's level launches fill the chip while another's ramp up or drain.
-    Outputs are allocated once for the whole batch on the caller's stream; each run writes
-    its slices; the caller's stream waits for every run.  Returns the level list or None."""
-    B, C, H, W = (int(v) for v in x.shape)
-    dev = x.device
-    main = torch.cuda.current_stream(dev)
-    sizes, h_, w_ = [], H, W
-    for _ in range(levels):
-        h_, w_ = h_ // 2, w_ // 2
-        sizes.append((h_, w_))
-    outs = [torch.empty((B, C, h, w), dtype=out_dtype, device=dev) for h, w in sizes]
-    bounds = [(g * B) // groups for g in range(groups + 1)]
-    fork = torch.cuda.Event()
-    fork.record(main)
-    streams = _side_streams(dev, groups)
-    ok = True
-    for g in range(groups):
-        s0, s1 = bounds[g], bounds[g + 1]
-        st = streams[g]
-        st.wait_event(fork)
-        with torch.cuda.stream(st):
-            cur = x[s0:s1]
-            for lv, (h1, w1) in enumerate(sizes):
-                y = ops.hex_pyramid_level(cur, conv.kernel, conv.bias, (h1, w1),
-                                          int(conv.even_odd_offset),
-                                          from_rect=(lv == 0 and l0_from_rect),
-                                          out_dtype=out_dtype, out=outs[lv][s0:s1])
-                if y is None:
-                    ok = False
-                    break
-                cur = y
-        x.record_stream(st)              # the caching allocator: used on st until it is done
-        for o in outs:
-            o.record_stream(st)
-        if not ok:
-            break
-    for g in range(groups):
-        main.wait_stream(streams[g])
-    return outs if ok else None
-
-
-def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=True, groups=None):
+def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=True):
     """Hex Gaussian pyramid (BASELINE config 5): rect -> hex at full size
     (geometry_np.py:358-519), then `levels` x [conv (a HexConv2d, HexFrames.py:96-169)
     -> hexresize to (h//2, w//2) (geometry_np.py:520-681)].  Returns the list of level
@@ -136,24 +81,15 @@ def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=True
     pass of hg_hex_pyramid_level with the intermediates in fp32 on chip; level 0 reads the
     rect image and makes rect -> hex on the fly (l0_from_rect, the streaming kernel's FR
     mode: 1.12 vs 1.29 ms for a separate rect -> hex pass on config 5, tools/ab_pyramid.py);
-    otherwise the operator chain, which stores every stage in out_dtype.  groups: the fused
-    levels run as that many runs of images on separate HIP streams (default: 2 for a batch of
-    >= 2 rect images; 1 = one stream); each level launch of a short pyramid pays a ramp and a
-    tail of 16-50 us (profiles/r06/launch_edges.txt), which the other run's work fills.
+    otherwise the operator chain, which stores every stage in out_dtype.  (Round 6 measured
+    the batch split into runs of images on 2 / 4 / 8 HIP streams to overlap the level
+    launches' ramps and tails: 4-13 % slower than one stream, profiles/r06/; not used.)
     """
     if out_dtype is None:
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
     H, W = x.shape[-2:]
     outs = []
     if fused and pyramid_fusable(conv) and not torch.is_grad_enabled():
-        if groups is None:
-            groups = 2 if (x.dim() == 4 and x.shape[0] >= 2 and l0_from_rect) else 1
-        groups = max(1, min(int(groups), int(x.shape[0]) if x.dim() == 4 else 1))
-        if groups > 1 and l0_from_rect and x.dim() == 4:
-            got = _pyramid_fused_groups(x.contiguous(), conv, levels, out_dtype, l0_from_rect,
-                                        groups)
-            if got is not None:
-                return got
         cur, h_, w_, ok = x, H, W, True
         if not l0_from_rect:
             cur = ops.rect_to_hex(x, (H, W), out_dtype=out_dtype)

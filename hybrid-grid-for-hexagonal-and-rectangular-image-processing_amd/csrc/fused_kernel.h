@@ -43,9 +43,10 @@ constexpr int FU_OWN = FU_OWN_;       // owned columns per 128-column window
 #define FU_RB_PYRS_ 24                // MD 5 (= MD 4 on short bands for small levels)
 #endif
 #ifndef FU_RB_RT_
-#define FU_RB_RT_ 12                  // MD 2: rows per band (66 -> 30: 0.321 -> 0.307 ms, r03 A/B;
-                                      // 30 -> 12 with the upward bands of round 6: -2.3 %, which
-                                      // also shortens the launch's tail, profiles/r06/)
+#define FU_RB_RT_ 6                   // MD 2: rows per band (66 -> 30: 0.321 -> 0.307 ms, r03 A/B;
+                                      // with the upward bands of round 6 shorter is faster: 30 /
+                                      // 12 / 6 rows 0.304 / 0.297 / 0.289 ms, and the launch's
+                                      // ramp + tail 42 -> 20 us at 12, profiles/r06/)
 #endif
 constexpr int FU_RB = FU_RB_;
 constexpr int FU_RB_CONV = FU_RB_CONV_;

@@ -197,23 +197,25 @@ def test_hex_pyramid_8k_batch8_first_last(monkeypatch):
             assert torch.equal(a[0], b[i])
 
 
-@pytest.mark.parametrize("B,groups", [(8, None), (8, 3), (5, 2), (3, 3)])
-def test_hex_pyramid_image_groups_on_streams_bit_identical(B, groups, monkeypatch):
-    """hex_pyramid's fused levels with the batch split into runs of images on separate HIP
-    streams (round 6; default 2 runs) write the same bits as one launch per level over the
-    whole batch: the work per image is the same kernel code, only the launches differ.  The
-    bench's 8 x 8K shape and uneven splits."""
+def test_pyramid_level_out_slices():
+    """hex_pyramid_level(out=) writes into slices of one batch output (round 6) the same bits
+    as separate calls, and rejects a wrong out."""
     conv = gaussian_conv()
-    gen = torch.Generator(device=DEV).manual_seed(10 + B)
-    H, W = (4320, 7680) if B == 8 else (272, 480)
-    x = torch.rand((B, 3, H, W), generator=gen, device=DEV, dtype=torch.float16)
-    ref = fused_levels_only(x, conv, monkeypatch)
+    gen = torch.Generator(device=DEV).manual_seed(21)
+    x = torch.rand((4, 3, 272, 480), generator=gen, device=DEV, dtype=torch.float16)
     with torch.no_grad():
-        got = hex_pyramid(x, conv, levels=3, groups=groups)
-        one = hex_pyramid(x, conv, levels=3, groups=1)
+        ref = ops.hex_pyramid_level(x, conv.kernel, None, (136, 240), 0, from_rect=True,
+                                    out_dtype=torch.float16)
+        out = torch.full((4, 3, 136, 240), float("nan"), device=DEV, dtype=torch.float16)
+        for s0 in (0, 2):
+            y = ops.hex_pyramid_level(x[s0:s0 + 2], conv.kernel, None, (136, 240), 0,
+                                      from_rect=True, out_dtype=torch.float16, out=out[s0:s0 + 2])
+            assert y.data_ptr() == out[s0:s0 + 2].data_ptr()
+        with pytest.raises(ValueError):
+            ops.hex_pyramid_level(x, conv.kernel, None, (136, 240), 0, from_rect=True,
+                                  out_dtype=torch.float16, out=out[:, :, :, :120])
     torch.cuda.synchronize()
-    for a, b, c in zip(got, ref, one):
-        assert a.shape == b.shape and torch.equal(a, b) and torch.equal(c, b)
+    assert torch.equal(out, ref)
 
 
 @pytest.mark.parametrize("H,W", [(540, 960), (136, 250)])

@@ -21,14 +21,23 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STAGES = {   # json key -> (prof_pipeline stage, kernel-name substring)
+STAGES = {   # json key -> (prof_pipeline stage, kernel-name substring[, algorithmic bytes])
     "pipeline_r2h_conv_h2r": ("fused", "k_fused"),
     "rect_to_hex": ("r2h", "k_r2h_stream"),
     "hexconv2d": ("conv", "k_fused"),           # HexConv2d 3->3 runs on k_fused MD 1
     "hex_to_rect": ("h2r", "k_h2r_stream"),
     "calib_torch_copy": ("copy", "__amd_rocclr_copyBuffer"),
     "calib_r2h_nearest": ("r2h_nearest", "k_resample_nearest"),
+    # round 6: the config-2 round trip and config-5 level 0, each on its own bytes
+    # (algorithmic read bytes, write bytes)
+    "pipeline_r2h_h2r": ("rt", "k_fused", (32 * 3 * 1080 * 1920 * 4, 32 * 3 * 1080 * 1920 * 4)),
+    "pyramid_level0_from_rect": ("pyr0", "k_fused", (8 * 3 * 4320 * 7680 * 2, 8 * 3 * 2160 * 3840 * 2)),
 }
+# The FETCH_SIZE x2 correction was calibrated at the headline kernel's own access width (8 B per
+# lane, dwordx2) in round 6: tools/microbench/walk8.hip's one-shot copy8 reads 1.0000x its bytes
+# (profiles/r06/walk8_pmc.txt), as the 16-B copy does.
+CAL_8B = {"copy8_fetch_x2_over_bytes": 1.0000, "copy16_fetch_x2_over_bytes": 1.0000,
+          "source": "profiles/r06/walk8_pmc.txt (tools/microbench/walk8.hip)"}
 
 
 def run_pass(out, stage, counter, batch):
@@ -63,7 +72,10 @@ def main():
     H, W, C = 2160, 3840, 3
     known = 2 * batch * C * H * W * 2        # one bf16 read + one bf16 write of the batch
     res = {}
-    for key, (stage, sub) in STAGES.items():
+    for key, spec in STAGES.items():
+        stage, sub = spec[0], spec[1]
+        alg_r, alg_w = spec[2] if len(spec) > 2 else (known / 2, known / 2)
+        alg = alg_r + alg_w
         dirs = [os.path.join(out, f"{stage}_{c}") if only else run_pass(out, stage, c, batch)
                 for c in ("FETCH_SIZE", "WRITE_SIZE")]
         f, nf = read(dirs[0], sub, "FETCH_SIZE")
@@ -72,8 +84,10 @@ def main():
         res[key] = {"FETCH_SIZE_KB": f, "WRITE_SIZE_KB": w, "dispatches": [nf, nw],
                     "read_bytes_corrected": fetch_b, "write_bytes": write_b,
                     "hbm_bytes_per_launch": fetch_b + write_b,
-                    "alg_bytes_per_launch": known,
-                    "traffic_over_alg": (fetch_b + write_b) / known}
+                    "alg_bytes_per_launch": alg,
+                    "traffic_over_alg": (fetch_b + write_b) / alg,
+                    "reads_over_alg_reads": fetch_b / alg_r,
+                    "writes_over_alg_writes": write_b / alg_w}
         print(key, json.dumps(res[key]), flush=True)
     sys.path[:0] = [os.path.join(ROOT, "hybrid-grid-for-hexagonal-and-rectangular-image-processing_amd")]
     from HyGrid._abi import kernel_source_digest
@@ -81,6 +95,7 @@ def main():
            "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, "
                      f"tools/prof_pipeline.py <stage> {batch} 2 (4K RGB bf16)",
            "correction": "bytes = KB x 1024; FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md §HBM)",
+           "calibration_8B_lanes": CAL_8B,
            "batch": batch, "kernels": res}
     with open(os.path.join(out, "pmc_traffic.json"), "w") as fh:
         json.dump(doc, fh, indent=1)

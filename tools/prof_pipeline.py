@@ -1,7 +1,8 @@
 """Profiling driver: runs one operator of the hot path a few times on a synthetic
 4K bf16 batch so that rocprofv3 (kernel trace / PMC passes) can attribute it.
 
-usage: python tools/prof_pipeline.py [fused|r2h|conv|h2r|r2h_nearest|copy] [batch] [iters]
+usage: python tools/prof_pipeline.py [fused|r2h|conv|h2r|r2h_nearest|copy|rt|pyr0] [batch] [iters]
+(rt and pyr0 use their own configs: 1080p fp32 b32, 8K fp16 b8)
 
 `copy` (torch bf16 clone) and `r2h_nearest` (one read + one write of every element) are
 the known-byte calibration runs for the FETCH_SIZE/WRITE_SIZE counters.
@@ -30,7 +31,7 @@ def main():
     conv = HexConv2d(3, 3, 0, 2, padding=1, bias=True).to(dev)
     conv.out_dtype = torch.bfloat16
     with torch.no_grad():
-        for _ in range(iters):
+        for _i in range(iters):
             if what == "fused":
                 rect_hex_conv_rect(x, conv, out_dtype=torch.bfloat16)
             elif what == "r2h":
@@ -43,6 +44,17 @@ def main():
                 ops.rect_to_hex(x, (H, W), interp=0)
             elif what == "copy":
                 x.clone()
+            elif what == "rt":          # config 2: 1080p RGB fp32 b32 round trip (k_fused MD 2)
+                if _i == 0:
+                    xr = torch.rand((32, 3, 1080, 1920), device=dev)
+                ops.pipeline_r2h_h2r(xr)
+            elif what == "pyr0":        # config 5 level 0: 8K RGB fp16 b8 from the rect image (MD 3)
+                if _i == 0:
+                    xp = torch.rand((8, 3, 4320, 7680), device=dev, dtype=torch.float16)
+                    kp = torch.tensor([1, 1, 1, 6, 1, 1, 1], dtype=torch.float32,
+                                      device=dev).div_(12).expand(3, 7).contiguous()
+                ops.hex_pyramid_level(xp, kp, None, (2160, 3840), 0, from_rect=True,
+                                      out_dtype=torch.float16)
             else:
                 raise SystemExit(f"unknown stage {what!r}")
     torch.cuda.synchronize()
