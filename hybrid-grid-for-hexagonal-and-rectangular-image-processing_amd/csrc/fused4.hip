@@ -10,9 +10,8 @@
 // here the neighbours of pair A are pair B's values (no DPP), the halo is 1/32 and the reads
 // ~1.04x; 8-B loads and stores per lane (walk6: the access pattern alone 0.615 -> 0.657 of
 // 8 TB/s at 42-row bands, 0.73 at 18-24; profiles/r04/walk6_b.txt).  Registers: 29 of the 32
-// weight pairs in SGPRs (102 SGPRs) and one rect row of prefetch keep it at 124 VGPRs, 4 waves
-// per SIMD (21 pairs / 2 rows ahead: 150 VGPRs, 3 waves; both 1-3 % faster than k_fused MD 0
-// in in-process A/Bs on three boxes, profiles/r04/f4/).
+// weight pairs in SGPRs (106 SGPRs) and two rect rows of prefetch: 136 VGPRs, 3 waves per SIMD
+// (round 6; one row of prefetch at 124 VGPRs and 4 waves was rounds 4-5's choice).
 //
 // Domain: fused_try's (same-size lattice, padding 1, value 0) with bf16 in and out, C = O = 3,
 // groups 1, w and w2 multiples of 4.  (Round 5 also built this layout for HexConv2d alone and
@@ -31,7 +30,10 @@ namespace hg {
 #define F4_RB_ 30                      // output rows per band (multiple of 6; 30 the most even across boxes: profiles/r04/f4)
 #endif
 #ifndef F4_PD
-#define F4_PD 1                        // rect rows loaded ahead of use (1..4): 1 fits 124 VGPRs
+#define F4_PD 2                        // rect rows loaded ahead of use (1..4): 2 at 136 VGPRs, 3
+                                       // waves per SIMD, is 0.9-2.1 % faster than 1 at 124 VGPRs
+                                       // and 4 waves once the odd bands walk upwards (round 6,
+                                       // profiles/r06/fused4_pd*_ab*.txt)
 #endif
 #ifndef F4_WPS
 #define F4_WPS 29                      // weight pairs in SGPRs (the rest in VGPRs): 102 SGPRs
@@ -40,7 +42,7 @@ namespace hg {
 #define F4_ORDER 0                     // workgroup order (A/B): 0 group fastest, 1 band fastest
 #endif
 #ifndef F4_WPE
-#define F4_WPE 4                       // waves per SIMD asked of the register allocator
+#define F4_WPE 3                       // waves per SIMD asked of the register allocator
 #endif
 #ifndef F4_REV
 #define F4_REV 1                       // odd full bands walk upwards (shared halo rows in L2, below)

@@ -783,9 +783,12 @@ void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
         {
             Raw t0[C], t1[C], t2[C];
             const unsigned o0 = row_off(row(-2)), o1 = row_off(row(-1)), o2 = row_off(row(0));
+            // MD 2 outputs u rows row(0) .. row(n-1) only: u row(-1) is not made, so rect row
+            // row(-2) is not needed (an out-of-range load: no memory access)
+            const unsigned xo0 = MD == 2 ? 0x80000000u : xoff;
     #pragma unroll
             for (int c = 0; c < C; ++c) {
-                t0[c] = fu_load<Tin>(xrs, xoff, o0 + c * xplane);
+                t0[c] = fu_load<Tin>(xrs, xo0, o0 + c * xplane);
                 t1[c] = fu_load<Tin>(xrs, xoff, o1 + c * xplane);
                 t2[c] = fu_load<Tin>(xrs, xoff, o2 + c * xplane);
             }
@@ -805,7 +808,8 @@ void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
                 XP[0][c] = fu_unpack2<Tin>(t2[c], hi16);   // row(0)  -> slot 0
             }
         }
-        urow(IC<-2>{}, lut[lut_e(-1)], std::false_type{}, std::false_type{});   // u row(-1): start only
+        if constexpr (MD != 2)
+            urow(IC<-2>{}, lut[lut_e(-1)], std::false_type{}, std::false_type{});   // u row(-1): start only
         convert(IC<1>{}, IC<1>{});                                              // row(1) -> slot 1
         urow(IC<-1>{}, lut[lut_e(0)], std::true_type{}, std::false_type{});     // u row(0): start, centre
         // Drain the prologue's loads: the compiler's wait counts at the loop header merge the
