@@ -302,6 +302,12 @@ def main():
         sys.exit(2)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    # stdout carries one line, the JSON result: from here on anything else written to fd 1 (RCCL
+    # prints a version banner to stdout when a communicator is created, at N = 1 too) goes to
+    # stderr, and the line goes to a duplicate of the original stdout
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -338,6 +344,9 @@ def main():
         gen = torch.Generator().manual_seed(2 + rank)
         x = torch.rand((B, C, H, W), generator=gen, dtype=torch.float32)
         conv = None
+        # test hook: rank r starts its pre-warm r x BENCH_DRY_SKEW_MS later, so the ranks'
+        # wall-clock budgets end at different times (tests/test_bench_launch.py)
+        skew = float(os.environ.get("BENCH_DRY_SKEW_MS", "0")) * 1e-3 * rank
 
         def run_fused(record, ev):
             if record:
@@ -432,17 +441,27 @@ def main():
     def prewarm(fn, ms):
         """Untimed steps (with the per-step collective) for `ms` of wall time: clock /
         power-state settle, and first-use costs (allocations, code-object loads) paid here
-        rather than as an idle gap right before the timed steps."""
+        rather than as an idle gap right before the timed steps.  Every rank runs the same
+        number of rounds of 8 steps (a MAX all-reduce of "my time is not up" after each round):
+        a per-rank wall-clock loop would let ranks run different numbers of collectives and
+        hang at N > 1."""
         if ms <= 0:
-            return
-        ev_ = []
+            return 0
+        ev_, n = [], 0
         with torch.no_grad():
             t_end = time.perf_counter() + ms * 1e-3
-            while time.perf_counter() < t_end:
+            while True:
                 for _ in range(8):
                     step_sums(fn(False, ev_))
+                n += 8
                 sync()
+                go = torch.tensor([1.0 if time.perf_counter() < t_end else 0.0],
+                                  dtype=torch.float64, device=cdev)
+                dist.all_reduce(go, op=dist.ReduceOp.MAX)
+                if go.item() == 0.0:
+                    break
         dist.barrier()
+        return n
 
     def measure_line(fn, steps):
         """A secondary line: 100 ms of untimed pre-warm of its own step and max(3, W) warmup
@@ -457,7 +476,14 @@ def main():
         return measure(fn, steps, max(3, args.warmup), collective=False)
 
     img_bytes = B * C * H * W * 2          # one bf16 batch tensor
-    prewarm(run_unfused if args.unfused else run_fused, args.prewarm_ms)
+    if dry and skew > 0:
+        time.sleep(skew)
+    n_pre = prewarm(run_unfused if args.unfused else run_fused, args.prewarm_ms)
+    # every rank's pre-warm step count (equal by construction; reported so a test can check)
+    pre_all = torch.zeros(world, dtype=torch.float64, device=cdev)
+    dist.all_gather_into_tensor(pre_all, torch.tensor([float(n_pre)], dtype=torch.float64,
+                                                      device=cdev))
+    prewarm_steps = [int(v) for v in pre_all.tolist()]
     if args.unfused:
         stages = ("rect_to_hex", "hexconv2d", "hex_to_rect")
         y, elapsed, sms = measure(run_unfused, args.steps, args.warmup)
@@ -549,7 +575,7 @@ def main():
 
         def run_pyramid(record, ev):
             """HyGrid.pipeline.hex_pyramid, the product entry: the fused levels (level 0 straight
-            from the rect image), one launch per level; HIP events around the whole step."""
+            from the rect image) as one chained launch; HIP events around the whole step."""
             if record:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 e[0].record()
@@ -608,12 +634,14 @@ def main():
         own_u = [Bp * C * 2 * v for v in own_u]
         pyramid = {"workload": "config5: 8K RGB fp16, r2h -> 3 x [depthwise Gaussian HexConv2d "
                                "-> hexresize /2]",
-                   "path": "HyGrid.pipeline.hex_pyramid: hg_hex_pyramid_level x 3 (conv + "
-                           "hexresize, fp32 on chip; level 0 reads the rect image: rect -> hex "
-                           "made on the fly)",
+                   "path": "HyGrid.pipeline.hex_pyramid: hg_hex_pyramid_chain, the 3 levels "
+                           "in one launch (conv + hexresize, fp32 on chip; level 0 reads the "
+                           "rect image: rect -> hex made on the fly; a level's bands start when "
+                           "the bands of the level before that wrote their input rows are done)",
                    "levels_run": {"ms_per_step": round(el_p1 / steps_p * 1e3, 4),
-                                  "what": "the three level calls with an event between kernels "
-                                          "(the per-level times below)"},
+                                  "what": "the same levels as one hg_hex_pyramid_level launch "
+                                          "each, an event between kernels (the per-level times "
+                                          "below)"},
                    "batch_per_gpu": Bp, "value": round(world * Bp * Hp * Wp * steps_p / el_p / 1e6, 1),
                    "unit": "Mpix/s", "ms_per_step": round(el_p / steps_p * 1e3, 4),
                    "dtype": "f16", "out_shape": list(levels[0]),
@@ -768,7 +796,7 @@ def main():
             metric = json.load(f)["metric"]
         line = {
             "metric": metric, "value": round(mpix, 1), "unit": "Mpix/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "prewarm_ms": args.prewarm_ms, "ms_per_step": round(ms_per_step, 4),
+            "steps": args.steps, "warmup": args.warmup, "prewarm_ms": args.prewarm_ms, "prewarm_steps": prewarm_steps, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic U[0,1) bf16 rasters generated on device, seed 2+rank; "
                     "HexConv2d weights torch.manual_seed(3) + reference init",
@@ -791,7 +819,7 @@ def main():
                             "value is not a measurement")
         if line["n_gpus"] != args.gpus:
             raise SystemExit(f"bench: n_gpus {line['n_gpus']} != --gpus {args.gpus}")
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=result_out, flush=True)
     dist.destroy_process_group()
 
 

@@ -75,6 +75,9 @@ SIGNATURES = {
     "hg_hex_pyramid_level": ([_vp, _vp, _int, _int] + [_i64] * 6 + [_vp, _vp, _int, _int, _vp],
                              _int),
     "hg_hex_pyramid_level_kernel": ([_int, _int] + [_i64] * 6 + [_int, _int], _int),
+    "hg_hex_pyramid_chain_workspace": ([_int, _i64, _i64], _i64),
+    "hg_hex_pyramid_chain": ([_vp, ctypes.POINTER(_vp), _int, _int] + [_i64] * 4 +
+                             [_vp, _vp, _int, _vp, _i64, _vp], _int),
     "hg_pipeline_r2h_h2r": ([_vp, _vp, _int, _int] + [_i64] * 5 + [_vp], _int),
     "hg_pipeline_r2h_conv_h2r": ([_vp, _vp, _vp, _vp, _int, _int] + [_i64] * 9 +
                                  [_int, _int, _int, _dbl, _vp], _int),

@@ -495,6 +495,56 @@ def pipeline_r2h_conv_h2r(x, kernel, bias, hex_size=None, rect_size=None, paddin
     return y
 
 
+# one zeroed int32 workspace per (device, stream) for hg_hex_pyramid_chain (every launch leaves
+# it zeroed; calls on one stream are ordered, so they can share it)
+_CHAIN_WS = {}
+
+
+def chain_workspace(device, stream, nbytes):
+    """The (device, stream)'s pyramid-chain workspace, at least nbytes, zeroed on creation."""
+    key = (device.index, int(stream.value or 0))
+    ws = _CHAIN_WS.get(key)
+    if ws is None or ws.numel() * 4 < nbytes:
+        ws = torch.zeros(max(nbytes // 4 + 1, 1024), dtype=torch.int32, device=device)
+        _CHAIN_WS[key] = ws
+    return ws
+
+
+def hex_pyramid_chain(x, taps, bias=None, levels=3, even_odd_offset=0):
+    """`levels` pyramid levels from the rect image x in ONE launch (hg_hex_pyramid_chain):
+    level 0 = hex_pyramid_level(x, from_rect=True), level l = hex_pyramid_level(level l - 1),
+    each (h // 2, w // 2) of the one before, all in x's dtype (16-bit), bit-identical to those
+    calls.  Returns the list of levels, or None outside the chain's domain (levels 2-3, C = 3,
+    every level on the fused kernel: the caller then runs the levels one launch each)."""
+    _abi.require_device(x)
+    while x.dim() < 4:
+        x = x.unsqueeze(0)
+    x = x.contiguous()
+    B, C, h, w = (int(s) for s in x.shape)
+    if x.dtype not in (torch.float16, torch.bfloat16) or not 2 <= levels <= 3:
+        return None
+    k = taps.detach().float().reshape(C, 7).contiguous()
+    b = bias.detach().float().contiguous() if bias is not None else None
+    outs, hl, wl = [], h, w
+    for _ in range(levels):
+        hl, wl = hl // 2, wl // 2
+        outs.append(torch.empty((B, C, hl, wl), dtype=x.dtype, device=x.device))
+    L = _abi.lib()
+    need = int(L.hg_hex_pyramid_chain_workspace(int(levels), B, h))
+    if need < 0:
+        _abi.check(need, "hg_hex_pyramid_chain_workspace")
+    st_ = _abi.stream_of(x)
+    ws = chain_workspace(x.device, st_, need)
+    ys = (ctypes.c_void_p * levels)(*[o.data_ptr() for o in outs])
+    st = L.hg_hex_pyramid_chain(_abi.ptr(x), ys, int(levels), _abi.dtype_code(x.dtype), B, C, h,
+                                w, _abi.ptr(k), _abi.ptr(b), int(even_odd_offset), _abi.ptr(ws),
+                                ws.numel() * 4, st_)
+    if st in (HG_EUNSUP, _abi.HG_EDTYPE):
+        return None
+    _abi.check(st, "hg_hex_pyramid_chain")
+    return outs
+
+
 def hex_pyramid_level(x, taps, bias=None, size=None, even_odd_offset=0, from_rect=False,
                       out_dtype=None, out=None):
     """One hex Gaussian pyramid level in one pass: hexresize(HexConv2d_depthwise(x))

@@ -81,15 +81,25 @@ def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=True
     pass of hg_hex_pyramid_level with the intermediates in fp32 on chip; level 0 reads the
     rect image and makes rect -> hex on the fly (l0_from_rect, the streaming kernel's FR
     mode: 1.12 vs 1.29 ms for a separate rect -> hex pass on config 5, tools/ab_pyramid.py);
-    otherwise the operator chain, which stores every stage in out_dtype.  (Round 6 measured
-    the batch split into runs of images on 2 / 4 / 8 HIP streams to overlap the level
-    launches' ramps and tails: 4-13 % slower than one stream, profiles/r06/; not used.)
+    otherwise the operator chain, which stores every stage in out_dtype.  Round 6: 2-3 levels
+    from the rect image in x's 16-bit dtype run as ONE launch (ops.hex_pyramid_chain: a level's
+    bands start as soon as the bands of the level before that wrote their input rows are done,
+    so the launches' ramps and tails overlap; bit-identical to the per-level launches).  (Round 6
+    also measured the batch split into runs of images on 2 / 4 / 8 HIP streams to overlap the
+    level launches' ramps and tails: 4-13 % slower than one stream, profiles/r06/; not used.)
     """
     if out_dtype is None:
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
     H, W = x.shape[-2:]
     outs = []
     if fused and pyramid_fusable(conv) and not torch.is_grad_enabled():
+        if l0_from_rect and x.dtype == out_dtype and 2 <= levels <= 3:
+            # every level in one launch (hg_hex_pyramid_chain, round 6); None outside its domain
+            outs = ops.hex_pyramid_chain(x, conv.kernel, conv.bias, levels,
+                                         int(conv.even_odd_offset))
+            if outs is not None:
+                return outs
+            outs = []
         cur, h_, w_, ok = x, H, W, True
         if not l0_from_rect:
             cur = ops.rect_to_hex(x, (H, W), out_dtype=out_dtype)

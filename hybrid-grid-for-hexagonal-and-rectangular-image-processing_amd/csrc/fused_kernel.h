@@ -289,13 +289,28 @@ __device__ __forceinline__ void fu_sfor(F&& f) {
 // while they run side by side on one XCD) instead of a band's walk apart.  MD 2's u rows and
 // outputs are the same either way; MD 1's conv rows sum their below taps first on an upward
 // band (the same products in another order).
-template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD = 0>
-// MD 1 with 16-bit input and output fits 128 VGPRs (4 waves per SIMD); an fp32 raw ring or
-// fp32 stores need more, and capping those at 128 spills to scratch inside the row loop.
-__global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(
-    (MD == 1 && sizeof(Tin) == 2 && sizeof(Tout) == 2) ? FU_WPE_CONV : FU_WPE)))
-void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
-             const float* __restrict__ bias, Tout* __restrict__ y, FusedGeom F) {
+// A workgroup's LDS (one struct, so that a kernel running bands of several modes with the same
+// PYR / O — the pyramid chain, pyramid_fused.hip — allocates it once).
+constexpr int FU_ZW = 130;
+constexpr int FU_NPT = FU_RB_PYR / 2 + 1;
+template <bool PYR, int O>
+struct FuShared {
+    // per-wave u-row table {a, b, c, -}: u[r] = a*x[r-1] + b*x[r] + c*x[r+1]
+    float4 lut[FU_GW][FU_LUT];
+    // PYR: the two conv rows an output row reads, per wave: [row][channel][col], cols
+    // 0..127 of the window + a zero at 128 (vertices outside the raster) and a pad
+    float zl[PYR ? FU_GW : 1][PYR ? 2 * O * FU_ZW : 1];
+    // PYR: per output row of the band {0.5 i_, i_f} and i_n (geometry_np.py:601-612)
+    double ptd[PYR ? FU_GW : 1][PYR ? FU_NPT : 1][2];
+    int pti[PYR ? FU_GW : 1][PYR ? FU_NPT : 1];
+};
+
+// One workgroup's work unit (image, band, group of 4 windows) = logical block `blk`.
+template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD>
+__device__ __forceinline__ void fu_band(const Tin* __restrict__ x, const float* __restrict__ kern,
+                                        const float* __restrict__ bias, Tout* __restrict__ y,
+                                        const FusedGeom& F, int64_t blk,
+                                        FuShared<(MD >= 3), O>& sh) {
     constexpr int CG = C / G, OG = O / G;
     constexpr int PD = FU_PD;
     constexpr bool PYR = MD >= 3;                 // hex-pyramid level (hexresize output stage)
@@ -308,16 +323,12 @@ void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
 
     // The 4 waves of a workgroup take 4 adjacent windows of one (image, band).
     constexpr int GW = FU_THREADS / 64;             // windows per group
-    // per-wave u-row table {a, b, c, -}: u[r] = a*x[r-1] + b*x[r] + c*x[r+1]
-    __shared__ float4 lut_all[GW][FU_LUT];
-    // PYR: the two conv rows an output row reads, per wave: [row][channel][col], cols
-    // 0..127 of the window + a zero at 128 (vertices outside the raster) and a pad
-    constexpr int ZW = 130;
-    __shared__ float zl_all[PYR ? GW : 1][PYR ? 2 * O * ZW : 1];
-    // PYR: per output row of the band {0.5 i_, i_f} and i_n (geometry_np.py:601-612)
-    constexpr int NPT = FU_RB_PYR / 2 + 1;
-    __shared__ double ptd_all[PYR ? GW : 1][PYR ? NPT : 1][2];
-    __shared__ int pti_all[PYR ? GW : 1][PYR ? NPT : 1];
+    constexpr int ZW = FU_ZW;
+    constexpr int NPT = FU_NPT;
+    auto& lut_all = sh.lut;
+    auto& zl_all = sh.zl;
+    auto& ptd_all = sh.ptd;
+    auto& pti_all = sh.pti;
     const int lane = threadIdx.x & 63;
     const int wslot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float4* const lut = lut_all[wslot];
@@ -325,7 +336,6 @@ void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
     if constexpr (PYR) {
         if (lane < 2 * O) zl[lane * ZW + 128] = 0.f;   // the zero vertex of every row block
     }
-    const int64_t blk = (int64_t)xcd_swizzle(blockIdx.x, gridDim.x);
     const int ngrp = (F.nwin + GW - 1) / GW;
     const int grp = (int)(blk % ngrp);
     const int64_t rest = blk / ngrp;
@@ -892,6 +902,18 @@ void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
         else if (cd == 2 && rc == 2) dir(IC<2>{}, IC<2>{});
         else dir(IC<0>{}, IC<0>{});
     }
+}
+
+// MD 1 with 16-bit input and output fits 128 VGPRs (4 waves per SIMD); an fp32 raw ring or
+// fp32 stores need more, and capping those at 128 spills to scratch inside the row loop.
+template <typename Tin, typename Tout, int C, int O, int G, int OP, int MD = 0>
+__global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(
+    (MD == 1 && sizeof(Tin) == 2 && sizeof(Tout) == 2) ? FU_WPE_CONV : FU_WPE)))
+void k_fused(const Tin* __restrict__ x, const float* __restrict__ kern,
+             const float* __restrict__ bias, Tout* __restrict__ y, FusedGeom F) {
+    __shared__ FuShared<(MD >= 3), O> sh;
+    fu_band<Tin, Tout, C, O, G, OP, MD>(x, kern, bias, y, F,
+                                        (int64_t)xcd_swizzle(blockIdx.x, gridDim.x), sh);
 }
 
 }  // namespace hg

@@ -93,10 +93,11 @@ static bool pf_r2h_ok(const Geom& g) {
     return true;
 }
 
-int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
-                  int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
-                  const float* bias, int even_odd_offset, int from_rect, hipStream_t st,
-                  bool dry) {
+// The level's geometry and mode (MD 3 from the rect image, MD 4 / 5 from a hex image), or
+// HG_EUNSUP outside the kernel's domain.  Shared by the one-level launch and the chain.
+static int pf_prepare(const void* src, int src_dtype, int dst_dtype, int64_t batch, int64_t C,
+                      int64_t h, int64_t w, int64_t h1, int64_t w1, int from_rect, FusedGeom& F,
+                      int& md) {
     if (C != 1 && C != 3) return HG_EUNSUP;
     if ((w & 1) || w < 2 || h < 2 || h1 < 1 || w1 < 1 || batch < 1) return HG_EUNSUP;
     if (src_dtype != HG_F16 && src_dtype != HG_BF16) return HG_EUNSUP;
@@ -107,7 +108,7 @@ int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int6
         return HG_EUNSUP;
     const Geom g = make_tri(h, w, h1, w1, 0.5);
     if (!pf_lattice_ok(g)) return HG_EUNSUP;
-    FusedGeom F = {};
+    F = {};
     F.B = batch;
     F.h = (int)h; F.w = (int)w;           // input (rect for MD 3, hex for MD 4)
     F.h1 = (int)h; F.w1 = (int)w;         // hex / conv image: same size
@@ -125,7 +126,7 @@ int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int6
     // the chip (256 CUs x 4 SIMDs x 4 waves) runs on short bands (MD 5): the last round of a
     // launch that is only a few rounds long is mostly idle.  A/B switch HYGRID_PYR_SHORT=0/1
     // (exactly "0" or "1"; anything else: the rule above).
-    int md = from_rect ? 3 : 4;
+    md = from_rect ? 3 : 4;
     if (!from_rect) {
         const int64_t waves = batch * ((h + fu_rb(4) - 1) / fu_rb(4)) * (int64_t)F.nwin;
         bool shrt = waves < 6 * 4096;
@@ -133,8 +134,19 @@ int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int6
         if (env_is("HYGRID_PYR_SHORT", "0")) shrt = false;
         if (shrt) md = 5;
     }
-    if (dry) return md == 5 ? HG_PYR_FUSED_SHORT : HG_PYR_FUSED;
     F.nband = (int)((h + fu_rb(md) - 1) / fu_rb(md));
+    return HG_OK;
+}
+
+int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int64_t batch,
+                  int64_t C, int64_t h, int64_t w, int64_t h1, int64_t w1, const float* taps,
+                  const float* bias, int even_odd_offset, int from_rect, hipStream_t st,
+                  bool dry) {
+    FusedGeom F;
+    int md = 0;
+    const int rc = pf_prepare(src, src_dtype, dst_dtype, batch, C, h, w, h1, w1, from_rect, F, md);
+    if (rc != HG_OK) return rc;
+    if (dry) return md == 5 ? HG_PYR_FUSED_SHORT : HG_PYR_FUSED;
     const int op = (even_odd_offset + 1) & 1;   // tap column class at padding 1
     if (src_dtype == HG_F16)
         return dst_dtype == HG_F32 ? pf_channels<_Float16, float>(src, taps, bias, dst, F, (int)C, md, op, st)
@@ -143,4 +155,185 @@ int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int6
                                : pf_channels<__bf16, __bf16>(src, taps, bias, dst, F, (int)C, md, op, st);
 }
 
+// ---- the pyramid chain: every level in one launch (round 6) ---------------------------------
+// One level per launch pays each launch's ramp and tail (profiles/r06/launch_edges.txt: 50-65,
+// 12-16 and 20-22 us of fixed cost for the three config-5 levels, 0.61 ms in all).  The chain
+// runs the levels' workgroups in one grid, level after level in block order, and a workgroup of
+// level l >= 1 starts its band once the bands of level l - 1 that wrote its input rows are
+// complete: per (image, band) of every producing level a counter of finished window groups.
+//   * Deadlock freedom: workgroups are dispatched in block order (per XCD, round robin), so
+//     every producer of a waiting workgroup was dispatched before it, and producers of level 0
+//     never wait.  A wait that outlasts PC_SPIN polls (~1 s) sets the workspace's fault word and
+//     goes on (wrong output, never a hang); the tests assert the word stays 0.
+//   * Visibility: a producer's waves release at agent scope (their output rows written back from
+//     the XCD's L2) before one thread adds 1 to the counter; a waiting workgroup acquires at
+//     agent scope after the counters are reached.
+//   * Each level's block count is a multiple of 8 and starts on a multiple of 8, so a block's
+//     XCD (blockIdx % 8) maps to the level's XCD-contiguous slice as in the one-level launch:
+//     an XCD walks image after image, band after band, so the first bands of level l + 1 start
+//     while the last ones of level l finish, mostly on the same XCD.
+//   * The last workgroup to finish (a done counter) zeroes the counters and the done count: the
+//     caller zeroes the workspace once, every launch leaves it zeroed (the fault word stays).
+constexpr int PC_MAXLEV = 3;
+constexpr int PC_SPIN = 1 << 20;
+struct PyrChain {
+    FusedGeom F[PC_MAXLEV];
+    const void* x[PC_MAXLEV];
+    void* y[PC_MAXLEV];
+    unsigned first[PC_MAXLEV];    // first block of each level (multiple of 8)
+    unsigned nblk[PC_MAXLEV];     // blocks of each level (multiple of 8)
+    int* cnt[PC_MAXLEV];          // level l's (image, band) counters, read by level l + 1
+    int* ws;                      // [0] done, [1] fault, [2 ...] the counters
+    int ncnt;                     // counters in all
+    int levels;
+};
+
+// workspace ints: done, fault, and B x nband counters of every level but the last
+static int64_t pc_ws_ints(int levels, int64_t batch, int64_t h) {
+    int64_t n = 2, hl = h;
+    for (int l = 0; l + 1 < levels; ++l) {
+        n += batch * ((hl + fu_rb(l == 0 ? 3 : 5) - 1) / fu_rb(l == 0 ? 3 : 5));
+        hl /= 2;
+    }
+    return n;
+}
+
+template <typename T, int C, int OP>
+__global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(FU_WPE)))
+void k_pyr_chain(const float* __restrict__ kern, const float* __restrict__ bias, PyrChain P) {
+    __shared__ FuShared<true, C> sh;
+    __shared__ int last;
+    const unsigned bid = blockIdx.x;
+    const int L = (P.levels > 2 && bid >= P.first[2]) ? 2 : (bid >= P.first[1] ? 1 : 0);   // uniform
+    const int64_t blk = (int64_t)xcd_swizzle(bid - (L == 2 ? P.first[2] : L == 1 ? P.first[1] : 0u),
+                                             L == 2 ? P.nblk[2] : L == 1 ? P.nblk[1] : P.nblk[0]);
+    if (L == 0) {
+        fu_band<T, T, C, C, C, OP, 3>((const T*)P.x[0], kern, bias, (T*)P.y[0], P.F[0], blk, sh);
+    } else {
+        // level L's geometry and buffers (selects on kernel arguments, no private copy)
+        const FusedGeom& F = L == 2 ? P.F[2] : P.F[1];
+        const FusedGeom& Fp = L == 2 ? P.F[1] : P.F[0];    // the producing level
+        int* const cnt = L == 2 ? P.cnt[1] : P.cnt[0];
+        const int ngrp = (F.nwin + FU_GW - 1) / FU_GW;
+        const int64_t rest = blk / ngrp;
+        const int band = (int)(rest % F.nband);
+        const int64_t b = rest / F.nband;
+        if (b < F.B) {
+            // input rows the band reads: row(-2) .. row(n + 1), clamped to the raster
+            const int s0 = band * fu_rb(5), s1 = min(s0 + fu_rb(5), F.h1);
+            const int lo = max(s0 - 2, 0), hi = min(s1 + 1, F.h - 1);
+            const int half = (L == 1 ? fu_rb(3) : fu_rb(5)) / 2;   // output rows per producer band
+            const int j0 = lo / half, j1 = min(hi / half, Fp.nband - 1);
+            const int pgrp = (Fp.nwin + FU_GW - 1) / FU_GW;
+            if ((int)threadIdx.x <= j1 - j0) {
+                int* const c = cnt + b * Fp.nband + j0 + threadIdx.x;
+                int it = 0;
+                while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pgrp) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++it >= PC_SPIN) {
+                        __hip_atomic_store(P.ws + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        const T* x = (const T*)(L == 2 ? P.x[2] : P.x[1]);
+        T* y = (T*)(L == 2 ? P.y[2] : P.y[1]);
+        fu_band<T, T, C, C, C, OP, 5>(x, kern, bias, y, F, blk, sh);
+    }
+    // this workgroup's band is complete: count it for the next level
+    if (L + 1 < P.levels) {
+        const FusedGeom& F = L == 1 ? P.F[1] : P.F[0];
+        const int ngrp = (F.nwin + FU_GW - 1) / FU_GW;
+        const int64_t rest = blk / ngrp;
+        const int64_t b = rest / F.nband;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+        if (threadIdx.x == 0 && b < F.B) {
+            int* const cnt = L == 1 ? P.cnt[1] : P.cnt[0];
+            __hip_atomic_fetch_add(cnt + b * F.nband + (int)(rest % F.nband), 1, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // the last workgroup of the launch zeroes the counters for the next one
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(P.ws, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+               (int)gridDim.x - 1;
+    __syncthreads();
+    if (last) {
+        for (int i = threadIdx.x; i < P.ncnt; i += FU_THREADS)
+            __hip_atomic_store(P.ws + 2 + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) __hip_atomic_store(P.ws, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+static int pc_run(const void* src, void* const* dsts, int levels, int dtype, int64_t batch,
+                  int64_t C, int64_t h, int64_t w, const float* taps, const float* bias,
+                  int even_odd_offset, void* workspace, int64_t ws_bytes, hipStream_t st) {
+    if (levels < 1 || batch < 0 || C < 1 || h < 1 || w < 1 || ws_bytes < 0) return HG_EINVAL;
+    if (even_odd_offset != 0 && even_odd_offset != 1) return HG_EINVAL;
+    if (dtype != HG_F16 && dtype != HG_BF16 && dtype != HG_F32) return HG_EDTYPE;
+    if (batch == 0) return HG_OK;
+    if (!src || !dsts || !taps) return HG_EINVAL;
+    for (int l = 0; l < levels; ++l)
+        if (!dsts[l]) return HG_EINVAL;
+    if (env_is("HYGRID_PYR_CHAIN", "0")) return HG_EUNSUP;   // A/B switch: one launch per level
+    if (levels < 2 || levels > PC_MAXLEV || C != 3 || dtype == HG_F32) return HG_EUNSUP;
+    PyrChain P = {};
+    P.levels = levels;
+    int64_t hl = h, wl = w, total = 0;
+    for (int l = 0; l < levels; ++l) {
+        int md = 0;
+        const int rc = pf_prepare(l ? dsts[l - 1] : src, dtype, dtype, batch, C, hl, wl, hl / 2,
+                                  wl / 2, l == 0, P.F[l], md);
+        if (rc != HG_OK) return rc;
+        if (md != (l == 0 ? 3 : 5)) return HG_EUNSUP;
+        P.x[l] = l ? dsts[l - 1] : src;
+        P.y[l] = dsts[l];
+        const int64_t nb = batch * (int64_t)P.F[l].nband * ((P.F[l].nwin + FU_GW - 1) / FU_GW);
+        P.first[l] = (unsigned)total;
+        P.nblk[l] = (unsigned)((nb + 7) / 8 * 8);
+        total += P.nblk[l];
+        if (total > INT_MAX) return HG_ESHAPE;
+        hl /= 2;
+        wl /= 2;
+    }
+    if (levels == 2) P.first[2] = UINT_MAX;
+    const int64_t need = pc_ws_ints(levels, batch, h);
+    if (!workspace || (reinterpret_cast<uintptr_t>(workspace) & 3) || ws_bytes < need * 4)
+        return HG_EINVAL;
+    P.ws = (int*)workspace;
+    P.ncnt = (int)(need - 2);
+    int* c = P.ws + 2;
+    for (int l = 0; l + 1 < levels; ++l) {
+        P.cnt[l] = c;
+        c += batch * P.F[l].nband;
+    }
+    const int op = (even_odd_offset + 1) & 1;   // tap column class at padding 1
+    const dim3 grid((unsigned)total), blk(FU_THREADS);
+    if (dtype == HG_F16) {
+        if (op) hipLaunchKernelGGL((k_pyr_chain<_Float16, 3, 1>), grid, blk, 0, st, taps, bias, P);
+        else hipLaunchKernelGGL((k_pyr_chain<_Float16, 3, 0>), grid, blk, 0, st, taps, bias, P);
+    } else {
+        if (op) hipLaunchKernelGGL((k_pyr_chain<__bf16, 3, 1>), grid, blk, 0, st, taps, bias, P);
+        else hipLaunchKernelGGL((k_pyr_chain<__bf16, 3, 0>), grid, blk, 0, st, taps, bias, P);
+    }
+    return launch_status();
+}
+
 }  // namespace hg
+
+extern "C" int64_t hg_hex_pyramid_chain_workspace(int levels, int64_t batch, int64_t h) {
+    if (levels < 1 || batch < 0 || h < 1) return HG_EINVAL;
+    return hg::pc_ws_ints(levels, batch, h) * 4;
+}
+
+extern "C" int hg_hex_pyramid_chain(const void* x, void* const* ys, int levels, int dtype,
+                                    int64_t batch, int64_t channels, int64_t h, int64_t w,
+                                    const float* taps, const float* bias, int even_odd_offset,
+                                    void* workspace, int64_t workspace_bytes, void* stream) {
+    return hg::pc_run(x, ys, levels, dtype, batch, channels, h, w, taps, bias, even_odd_offset,
+                      workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+}

@@ -286,6 +286,29 @@ int hg_hex_pyramid_level_kernel(int x_dtype, int y_dtype, int64_t batch, int64_t
                                 int64_t h, int64_t w, int64_t h1, int64_t w1, int even_odd_offset,
                                 int from_rect);
 
+/* Several pyramid levels in ONE launch (round 6): ys[l] = level l of the chain
+ *   ys[0] = hg_hex_pyramid_level(x, from_rect = 1, (h/2, w/2)),
+ *   ys[l] = hg_hex_pyramid_level(ys[l-1], from_rect = 0, (h_l/2, w_l/2))   (same taps / bias)
+ * — the chain the reference's user code builds from rect_to_hex_resample (geometry_np.py:358-519),
+ * HexConv2d (HexFrames.py:96-169) and hexresize (geometry_np.py:520-681) — bit-identical to those
+ * per-level calls, with the levels' workgroups in one grid: a band of level l starts when the
+ * bands of level l - 1 that wrote its input rows are complete (per-band counters in `workspace`),
+ * so the launches' ramps and tails overlap the neighbouring level's work.  x: (B, C, h, w) rect;
+ * ys[l]: (B, C, h >> (l+1), w >> (l+1)), all of `dtype` (F16 or BF16).  workspace: >=
+ * hg_hex_pyramid_chain_workspace(levels, batch, h) bytes, 4-byte aligned, ZEROED by the caller
+ * before its first use; every launch leaves it zeroed, except int [1], a fault word set to 1 if
+ * a workgroup waited longer than ~1 s for its input (output then invalid; not expected: the
+ * tests assert it stays 0).  One workspace per call in flight.  Returns HG_EUNSUP outside the
+ * chain's domain (levels 2-3, C = 3, 16-bit, level 0 on the fused kernel's MD 3 and the later
+ * levels on its short bands, i.e. the hg_hex_pyramid_level_kernel answers HG_PYR_FUSED then
+ * HG_PYR_FUSED_SHORT; HYGRID_PYR_CHAIN=0 also declines): then call hg_hex_pyramid_level per
+ * level. */
+int64_t hg_hex_pyramid_chain_workspace(int levels, int64_t batch, int64_t h);
+int hg_hex_pyramid_chain(const void* x, void* const* ys, int levels, int dtype, int64_t batch,
+                         int64_t channels, int64_t h, int64_t w, const float* taps,
+                         const float* bias, int even_odd_offset, void* workspace,
+                         int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

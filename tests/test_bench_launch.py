@@ -29,8 +29,10 @@ def _run(args, env, timeout=240):
 
 
 def _line(out):
-    lines = [ln for ln in out.strip().splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, out       # rank 0 prints exactly one JSON line
+    lines = [ln for ln in out.strip().splitlines() if ln.strip()]
+    # stdout is exactly one JSON line (rank 0's); library banners (RCCL's version lines at
+    # communicator creation) and logs go to stderr
+    assert len(lines) == 1 and lines[0].startswith("{"), out
     return json.loads(lines[0])
 
 
@@ -58,3 +60,16 @@ def test_world_size_must_match_gpus():
 def test_gpus_must_be_positive():
     r = _run(["--gpus", "0", "--dry-run"], _env(), timeout=120)
     assert r.returncode == 2
+
+
+def test_prewarm_runs_the_same_collectives_on_every_rank():
+    """The pre-warm runs for a wall-clock budget with the per-step collective inside: ranks of
+    different speed must still run the same number of steps (round 6: a per-rank time loop ran
+    different numbers of all-gathers: a hang at N = 2 was seen once under gloo, and RCCL
+    hangs on it).  Rank 1 starts its budget 40 ms later; the line reports every rank's count."""
+    r = _run(["--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1", "--prewarm-ms", "60"],
+             _env(BENCH_DRY_SKEW_MS="40"), timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2
+    assert len(d["prewarm_steps"]) == 2 and d["prewarm_steps"][0] == d["prewarm_steps"][1] > 0

@@ -3,6 +3,7 @@ hg_rect_to_hex / hg_hex_to_rect / hg_hexresize pick for the lattices of the refe
 entry points (hg_resample_kernel: the dispatch without a launch).  The GPU parity tests
 compare those kernels with the general ones (tests/test_gpu_down.py, test_gpu_stream.py);
 this pins that the specialised kernel is the one they exercise."""
+import ctypes
 import os
 
 import pytest
@@ -149,3 +150,25 @@ def test_pyramid_levels_take_the_fused_row_walk():
     # > 2x downsampling overflows every tile: declined up front by the exact host bound
     assert _pyr(F32, F32, 1, 3, 540, 960, 100, 180, 0, 0) == _abi.HG_EUNSUP
     assert _pyr(_abi.HG_U8, F32, 1, 3, 64, 64, 32, 32, 0, 0) == -2   # HG_EDTYPE
+
+
+def test_pyramid_chain_workspace_and_validation():
+    """hg_hex_pyramid_chain's host side (no launch): the workspace is 2 ints (done, fault) plus
+    one counter per (image, band) of every level but the last (level 0 on 60-row bands of the
+    conv image, later levels on 24-row bands), and argument errors return before any HIP call."""
+    L = _abi.lib()
+    # config 5: 8 x 4320-row images, 3 levels: 8 * 72 + 8 * 90 counters
+    assert L.hg_hex_pyramid_chain_workspace(3, 8, 4320) == 4 * (2 + 8 * 72 + 8 * 90)
+    assert L.hg_hex_pyramid_chain_workspace(2, 1, 70) == 4 * (2 + 2)
+    assert L.hg_hex_pyramid_chain_workspace(1, 4, 100) == 4 * 2
+    assert L.hg_hex_pyramid_chain_workspace(0, 4, 100) == _abi.HG_EINVAL
+    fake = ctypes.c_void_p(16)
+    ys = (ctypes.c_void_p * 3)(16, 16, 16)
+    args = [fake, ys, 3, _abi.HG_F16, 2, 3, 136, 250, fake, None]
+    assert L.hg_hex_pyramid_chain(fake, ys, 0, _abi.HG_F16, 2, 3, 136, 250, fake, None, 0, fake,
+                                  64, None) == _abi.HG_EINVAL
+    assert L.hg_hex_pyramid_chain(*args, 2, fake, 64, None) == _abi.HG_EINVAL   # offset class
+    assert L.hg_hex_pyramid_chain(fake, ys, 3, _abi.HG_U8, 2, 3, 136, 250, fake, None, 0, fake,
+                                  64, None) == _abi.HG_EDTYPE
+    assert L.hg_hex_pyramid_chain(None, None, 3, _abi.HG_F16, 0, 3, 136, 250, None, None, 0,
+                                  None, 0, None) == _abi.HG_OK                  # nothing to do
