@@ -575,7 +575,7 @@ def main():
 
         def run_pyramid(record, ev):
             """HyGrid.pipeline.hex_pyramid, the product entry: the fused levels (level 0 straight
-            from the rect image) as one chained launch; HIP events around the whole step."""
+            from the rect image), one launch per level; HIP events around the whole step."""
             if record:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 e[0].record()
@@ -634,10 +634,9 @@ def main():
         own_u = [Bp * C * 2 * v for v in own_u]
         pyramid = {"workload": "config5: 8K RGB fp16, r2h -> 3 x [depthwise Gaussian HexConv2d "
                                "-> hexresize /2]",
-                   "path": "HyGrid.pipeline.hex_pyramid: hg_hex_pyramid_chain, the 3 levels "
-                           "in one launch (conv + hexresize, fp32 on chip; level 0 reads the "
-                           "rect image: rect -> hex made on the fly; a level's bands start when "
-                           "the bands of the level before that wrote their input rows are done)",
+                   "path": "HyGrid.pipeline.hex_pyramid: hg_hex_pyramid_level x 3 (conv + "
+                           "hexresize, fp32 on chip; level 0 reads the rect image: rect -> hex "
+                           "made on the fly)",
                    "levels_run": {"ms_per_step": round(el_p1 / steps_p * 1e3, 4),
                                   "what": "the same levels as one hg_hex_pyramid_level launch "
                                           "each, an event between kernels (the per-level times "

@@ -495,17 +495,18 @@ def pipeline_r2h_conv_h2r(x, kernel, bias, hex_size=None, rect_size=None, paddin
     return y
 
 
-# one zeroed int32 workspace per (device, stream) for hg_hex_pyramid_chain (every launch leaves
-# it zeroed; calls on one stream are ordered, so they can share it)
+# one int32 workspace per (device, stream) for hg_hex_pyramid_chain (each call zeroes it on the
+# stream first; calls on one stream are ordered, so they can share it)
 _CHAIN_WS = {}
 
 
 def chain_workspace(device, stream, nbytes):
-    """The (device, stream)'s pyramid-chain workspace, at least nbytes, zeroed on creation."""
+    """The (device, stream)'s pyramid-chain workspace, at least nbytes (int [1] after a call:
+    the chain's fault word, 0 unless a workgroup waited > ~1 s for its input)."""
     key = (device.index, int(stream.value or 0))
     ws = _CHAIN_WS.get(key)
     if ws is None or ws.numel() * 4 < nbytes:
-        ws = torch.zeros(max(nbytes // 4 + 1, 1024), dtype=torch.int32, device=device)
+        ws = torch.zeros(max(nbytes // 4 + 4, 1024), dtype=torch.int32, device=device)
         _CHAIN_WS[key] = ws
     return ws
 

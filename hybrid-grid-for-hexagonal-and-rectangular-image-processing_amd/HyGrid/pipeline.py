@@ -8,6 +8,8 @@ rect_to_hex_resample (geometry_np.py:358-519) -> HexConvModule / HexConv2d
 whenever the geometry is near-identity and the layer is a plain radius-2,
 stride-1, constant-padded HexConv2d; otherwise the three HIP operators.
 """
+import os
+
 import torch
 
 from . import ops
@@ -81,20 +83,21 @@ def hex_pyramid(x, conv, levels=3, out_dtype=None, fused=True, l0_from_rect=True
     pass of hg_hex_pyramid_level with the intermediates in fp32 on chip; level 0 reads the
     rect image and makes rect -> hex on the fly (l0_from_rect, the streaming kernel's FR
     mode: 1.12 vs 1.29 ms for a separate rect -> hex pass on config 5, tools/ab_pyramid.py);
-    otherwise the operator chain, which stores every stage in out_dtype.  Round 6: 2-3 levels
-    from the rect image in x's 16-bit dtype run as ONE launch (ops.hex_pyramid_chain: a level's
-    bands start as soon as the bands of the level before that wrote their input rows are done,
-    so the launches' ramps and tails overlap; bit-identical to the per-level launches).  (Round 6
-    also measured the batch split into runs of images on 2 / 4 / 8 HIP streams to overlap the
-    level launches' ramps and tails: 4-13 % slower than one stream, profiles/r06/; not used.)
+    otherwise the operator chain, which stores every stage in out_dtype.  Round 6 measured two
+    ways of hiding the level launches' ramps and tails, both slower and not the default: the
+    levels in ONE launch (ops.hex_pyramid_chain, bit-identical; its inter-workgroup hand-off
+    costs 2.7x the per-level time; opt in with HYGRID_PYR_CHAIN=1) and the batch split into
+    runs of images on 2 / 4 / 8 HIP streams (4-13 % slower than one stream); profiles/r06/.
     """
     if out_dtype is None:
         out_dtype = x.dtype if x.dtype in (torch.bfloat16, torch.float16) else torch.float32
     H, W = x.shape[-2:]
     outs = []
     if fused and pyramid_fusable(conv) and not torch.is_grad_enabled():
-        if l0_from_rect and x.dtype == out_dtype and 2 <= levels <= 3:
-            # every level in one launch (hg_hex_pyramid_chain, round 6); None outside its domain
+        if (os.environ.get("HYGRID_PYR_CHAIN") == "1" and l0_from_rect and x.dtype == out_dtype
+                and 2 <= levels <= 3):
+            # opt-in: every level in one launch (hg_hex_pyramid_chain, round 6; measured 2.7x
+            # slower than one launch per level, DESIGN.md 7); None outside its domain
             outs = ops.hex_pyramid_chain(x, conv.kernel, conv.bias, levels,
                                          int(conv.even_odd_offset))
             if outs is not None:

@@ -158,55 +158,60 @@ int pyr_fused_try(const void* src, void* dst, int src_dtype, int dst_dtype, int6
 // ---- the pyramid chain: every level in one launch (round 6) ---------------------------------
 // One level per launch pays each launch's ramp and tail (profiles/r06/launch_edges.txt: 50-65,
 // 12-16 and 20-22 us of fixed cost for the three config-5 levels, 0.61 ms in all).  The chain
-// runs the levels' workgroups in one grid, level after level in block order, and a workgroup of
-// level l >= 1 starts its band once the bands of level l - 1 that wrote its input rows are
-// complete: per (image, band) of every producing level a counter of finished window groups.
-//   * Deadlock freedom: workgroups are dispatched in block order (per XCD, round robin), so
-//     every producer of a waiting workgroup was dispatched before it, and producers of level 0
-//     never wait.  A wait that outlasts PC_SPIN polls (~1 s) sets the workspace's fault word and
-//     goes on (wrong output, never a hang); the tests assert the word stays 0.
-//   * Visibility: a producer's waves release at agent scope (their output rows written back from
-//     the XCD's L2) before one thread adds 1 to the counter; a waiting workgroup acquires at
-//     agent scope after the counters are reached.
-//   * Each level's block count is a multiple of 8 and starts on a multiple of 8, so a block's
-//     XCD (blockIdx % 8) maps to the level's XCD-contiguous slice as in the one-level launch:
-//     an XCD walks image after image, band after band, so the first bands of level l + 1 start
-//     while the last ones of level l finish, mostly on the same XCD.
-//   * The last workgroup to finish (a done counter) zeroes the counters and the done count: the
-//     caller zeroes the workspace once, every launch leaves it zeroed (the fault word stays).
+// runs the levels' workgroups in one grid and a workgroup of level l >= 1 starts its band once
+// the bands of level l - 1 that wrote its input rows are complete: per (image, band) of every
+// producing level a counter of finished window groups.  The hand-off follows the agent-scope
+// release / acquire protocol of cdna_hip_programming.md Guideline 16 (no dispatch-order, timing
+// or placement assumption):
+//   * Work order by ticket: each workgroup draws a ticket (agent atomic) when it starts; tickets
+//     0 .. n0 - 1 are level 0's units, then level 1's, then level 2's.  A unit waits only on units
+//     of the level before, whose tickets are lower, so their workgroups have started (they are
+//     resident or done) and level 0 never waits: no deadlock whatever the dispatch order.  A wait
+//     past PC_SPIN polls (~1 s) sets the fault word and goes on (wrong output, never a hang; the
+//     tests assert the word is 0).  Within a level the ticket maps through the XCD swizzle (for
+//     L2 locality only, as in the one-level launch).
+//   * Producer: plain stores; every wave s_waitcnt vmcnt(0); barrier; one lane releases at agent
+//     scope (L2 write-back), waits, adds 1 to its band's counter (relaxed, agent).
+//   * Consumer: wave 0 polls the counters it needs (relaxed, s_sleep between polls), one lane
+//     acquires at agent scope and waits; barrier; then the band's plain loads.
+//   * The workspace words (ticket, fault, counters) are zeroed by a memset on the stream before
+//     every launch (Guideline 16: re-initialise every call).
 constexpr int PC_MAXLEV = 3;
 constexpr int PC_SPIN = 1 << 20;
 struct PyrChain {
     FusedGeom F[PC_MAXLEV];
     const void* x[PC_MAXLEV];
     void* y[PC_MAXLEV];
-    unsigned first[PC_MAXLEV];    // first block of each level (multiple of 8)
-    unsigned nblk[PC_MAXLEV];     // blocks of each level (multiple of 8)
+    unsigned first[PC_MAXLEV];    // first ticket of each level
+    unsigned nblk[PC_MAXLEV];     // units (workgroups) of each level
     int* cnt[PC_MAXLEV];          // level l's (image, band) counters, read by level l + 1
-    int* ws;                      // [0] done, [1] fault, [2 ...] the counters
-    int ncnt;                     // counters in all
+    int* ws;                      // [0] ticket, [1] fault, [2 ...] the counters
     int levels;
 };
 
-// workspace ints: done, fault, and B x nband counters of every level but the last
+// workspace ints: ticket, fault, and B x nband counters of every level but the last; padded to
+// a multiple of 4 ints (the per-call memset zeroes whole 16-byte blocks)
 static int64_t pc_ws_ints(int levels, int64_t batch, int64_t h) {
     int64_t n = 2, hl = h;
     for (int l = 0; l + 1 < levels; ++l) {
         n += batch * ((hl + fu_rb(l == 0 ? 3 : 5) - 1) / fu_rb(l == 0 ? 3 : 5));
         hl /= 2;
     }
-    return n;
+    return (n + 3) / 4 * 4;
 }
 
 template <typename T, int C, int OP>
 __global__ __launch_bounds__(FU_THREADS) __attribute__((amdgpu_waves_per_eu(FU_WPE)))
 void k_pyr_chain(const float* __restrict__ kern, const float* __restrict__ bias, PyrChain P) {
     __shared__ FuShared<true, C> sh;
-    __shared__ int last;
-    const unsigned bid = blockIdx.x;
-    const int L = (P.levels > 2 && bid >= P.first[2]) ? 2 : (bid >= P.first[1] ? 1 : 0);   // uniform
-    const int64_t blk = (int64_t)xcd_swizzle(bid - (L == 2 ? P.first[2] : L == 1 ? P.first[1] : 0u),
-                                             L == 2 ? P.nblk[2] : L == 1 ? P.nblk[1] : P.nblk[0]);
+    __shared__ unsigned tk;
+    if (threadIdx.x == 0)
+        tk = __hip_atomic_fetch_add((unsigned*)P.ws, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned t = tk;
+    const int L = (P.levels > 2 && t >= P.first[2]) ? 2 : (t >= P.first[1] ? 1 : 0);   // uniform
+    const unsigned n = L == 2 ? P.nblk[2] : L == 1 ? P.nblk[1] : P.nblk[0];
+    const int64_t blk = (int64_t)xcd_swizzle(t - (L == 2 ? P.first[2] : L == 1 ? P.first[1] : 0u), n);
     if (L == 0) {
         fu_band<T, T, C, C, C, OP, 3>((const T*)P.x[0], kern, bias, (T*)P.y[0], P.F[0], blk, sh);
     } else {
@@ -225,47 +230,42 @@ void k_pyr_chain(const float* __restrict__ kern, const float* __restrict__ bias,
             const int half = (L == 1 ? fu_rb(3) : fu_rb(5)) / 2;   // output rows per producer band
             const int j0 = lo / half, j1 = min(hi / half, Fp.nband - 1);
             const int pgrp = (Fp.nwin + FU_GW - 1) / FU_GW;
-            if ((int)threadIdx.x <= j1 - j0) {
-                int* const c = cnt + b * Fp.nband + j0 + threadIdx.x;
-                int it = 0;
-                while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pgrp) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++it >= PC_SPIN) {
-                        __hip_atomic_store(P.ws + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
+            if (threadIdx.x < 64) {                               // wave 0 polls, one lane per band
+                if ((int)threadIdx.x <= j1 - j0) {
+                    int* const c = cnt + b * Fp.nband + j0 + threadIdx.x;
+                    int it = 0;
+                    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pgrp) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++it >= PC_SPIN) {
+                            __hip_atomic_store(P.ws + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
                     }
                 }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU's L1 invalidated
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             __syncthreads();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         const T* x = (const T*)(L == 2 ? P.x[2] : P.x[1]);
         T* y = (T*)(L == 2 ? P.y[2] : P.y[1]);
         fu_band<T, T, C, C, C, OP, 5>(x, kern, bias, y, F, blk, sh);
     }
-    // this workgroup's band is complete: count it for the next level
+    // this workgroup's band is complete: publish it to the next level
     if (L + 1 < P.levels) {
         const FusedGeom& F = L == 1 ? P.F[1] : P.F[0];
         const int ngrp = (F.nwin + FU_GW - 1) / FU_GW;
         const int64_t rest = blk / ngrp;
         const int64_t b = rest / F.nband;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // every wave: its stores done
         __syncthreads();
         if (threadIdx.x == 0 && b < F.B) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the XCD's L2 written back
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             int* const cnt = L == 1 ? P.cnt[1] : P.cnt[0];
-            __hip_atomic_fetch_add(cnt + b * F.nband + (int)(rest % F.nband), 1, __ATOMIC_RELEASE,
+            __hip_atomic_fetch_add(cnt + b * F.nband + (int)(rest % F.nband), 1, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
-    }
-    // the last workgroup of the launch zeroes the counters for the next one
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(P.ws, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-               (int)gridDim.x - 1;
-    __syncthreads();
-    if (last) {
-        for (int i = threadIdx.x; i < P.ncnt; i += FU_THREADS)
-            __hip_atomic_store(P.ws + 2 + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (threadIdx.x == 0) __hip_atomic_store(P.ws, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -279,7 +279,6 @@ static int pc_run(const void* src, void* const* dsts, int levels, int dtype, int
     if (!src || !dsts || !taps) return HG_EINVAL;
     for (int l = 0; l < levels; ++l)
         if (!dsts[l]) return HG_EINVAL;
-    if (env_is("HYGRID_PYR_CHAIN", "0")) return HG_EUNSUP;   // A/B switch: one launch per level
     if (levels < 2 || levels > PC_MAXLEV || C != 3 || dtype == HG_F32) return HG_EUNSUP;
     PyrChain P = {};
     P.levels = levels;
@@ -294,7 +293,7 @@ static int pc_run(const void* src, void* const* dsts, int levels, int dtype, int
         P.y[l] = dsts[l];
         const int64_t nb = batch * (int64_t)P.F[l].nband * ((P.F[l].nwin + FU_GW - 1) / FU_GW);
         P.first[l] = (unsigned)total;
-        P.nblk[l] = (unsigned)((nb + 7) / 8 * 8);
+        P.nblk[l] = (unsigned)nb;
         total += P.nblk[l];
         if (total > INT_MAX) return HG_ESHAPE;
         hl /= 2;
@@ -302,16 +301,17 @@ static int pc_run(const void* src, void* const* dsts, int levels, int dtype, int
     }
     if (levels == 2) P.first[2] = UINT_MAX;
     const int64_t need = pc_ws_ints(levels, batch, h);
-    if (!workspace || (reinterpret_cast<uintptr_t>(workspace) & 3) || ws_bytes < need * 4)
+    if (!workspace || (reinterpret_cast<uintptr_t>(workspace) & 15) || ws_bytes < need * 4)
         return HG_EINVAL;
     P.ws = (int*)workspace;
-    P.ncnt = (int)(need - 2);
     int* c = P.ws + 2;
     for (int l = 0; l + 1 < levels; ++l) {
         P.cnt[l] = c;
         c += batch * P.F[l].nband;
     }
     const int op = (even_odd_offset + 1) & 1;   // tap column class at padding 1
+    const int ms = hip_status(hipMemsetAsync(workspace, 0, (size_t)need * 4, st));
+    if (ms != HG_OK) return ms;
     const dim3 grid((unsigned)total), blk(FU_THREADS);
     if (dtype == HG_F16) {
         if (op) hipLaunchKernelGGL((k_pyr_chain<_Float16, 3, 1>), grid, blk, 0, st, taps, bias, P);

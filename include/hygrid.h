@@ -295,14 +295,17 @@ int hg_hex_pyramid_level_kernel(int x_dtype, int y_dtype, int64_t batch, int64_t
  * bands of level l - 1 that wrote its input rows are complete (per-band counters in `workspace`),
  * so the launches' ramps and tails overlap the neighbouring level's work.  x: (B, C, h, w) rect;
  * ys[l]: (B, C, h >> (l+1), w >> (l+1)), all of `dtype` (F16 or BF16).  workspace: >=
- * hg_hex_pyramid_chain_workspace(levels, batch, h) bytes, 4-byte aligned, ZEROED by the caller
- * before its first use; every launch leaves it zeroed, except int [1], a fault word set to 1 if
- * a workgroup waited longer than ~1 s for its input (output then invalid; not expected: the
- * tests assert it stays 0).  One workspace per call in flight.  Returns HG_EUNSUP outside the
+ * hg_hex_pyramid_chain_workspace(levels, batch, h) bytes, 16-byte aligned; the call zeroes it
+ * on `stream` before the launch (the ticket, fault and per-band counter words), and after the
+ * launch int [1] is a fault word, 1 if a workgroup waited longer than ~1 s for its input
+ * (output then invalid; not expected: the tests assert 0).  One workspace per call in flight.
+ * Returns HG_EUNSUP outside the
  * chain's domain (levels 2-3, C = 3, 16-bit, level 0 on the fused kernel's MD 3 and the later
  * levels on its short bands, i.e. the hg_hex_pyramid_level_kernel answers HG_PYR_FUSED then
- * HG_PYR_FUSED_SHORT; HYGRID_PYR_CHAIN=0 also declines): then call hg_hex_pyramid_level per
- * level. */
+ * HG_PYR_FUSED_SHORT): then call hg_hex_pyramid_level per level.  Measured 2.7x slower than
+ * the per-level launches on config 5 (the hand-off's release / acquire / ticket costs exceed
+ * the launch edges it hides): HyGrid's hex_pyramid uses it only with
+ * HYGRID_PYR_CHAIN=1. */
 int64_t hg_hex_pyramid_chain_workspace(int levels, int64_t batch, int64_t h);
 int hg_hex_pyramid_chain(const void* x, void* const* ys, int levels, int dtype, int64_t batch,
                          int64_t channels, int64_t h, int64_t w, const float* taps,

@@ -153,14 +153,15 @@ def test_pyramid_levels_take_the_fused_row_walk():
 
 
 def test_pyramid_chain_workspace_and_validation():
-    """hg_hex_pyramid_chain's host side (no launch): the workspace is 2 ints (done, fault) plus
-    one counter per (image, band) of every level but the last (level 0 on 60-row bands of the
-    conv image, later levels on 24-row bands), and argument errors return before any HIP call."""
+    """hg_hex_pyramid_chain's host side (no launch): the workspace is 2 ints (ticket, fault)
+    plus one counter per (image, band) of every level but the last (level 0 on 60-row bands of
+    the conv image, later levels on 24-row bands), padded to whole 16-byte blocks, and argument
+    errors return before any HIP call."""
     L = _abi.lib()
     # config 5: 8 x 4320-row images, 3 levels: 8 * 72 + 8 * 90 counters
-    assert L.hg_hex_pyramid_chain_workspace(3, 8, 4320) == 4 * (2 + 8 * 72 + 8 * 90)
-    assert L.hg_hex_pyramid_chain_workspace(2, 1, 70) == 4 * (2 + 2)
-    assert L.hg_hex_pyramid_chain_workspace(1, 4, 100) == 4 * 2
+    assert L.hg_hex_pyramid_chain_workspace(3, 8, 4320) == 4 * 1300      # 2 + 576 + 720 -> 1300
+    assert L.hg_hex_pyramid_chain_workspace(2, 1, 70) == 4 * 4
+    assert L.hg_hex_pyramid_chain_workspace(1, 4, 100) == 4 * 4
     assert L.hg_hex_pyramid_chain_workspace(0, 4, 100) == _abi.HG_EINVAL
     fake = ctypes.c_void_p(16)
     ys = (ctypes.c_void_p * 3)(16, 16, 16)

@@ -1,5 +1,5 @@
 """Config 5 (8K fp16 b8, 3 fused pyramid levels): the levels as ONE chained launch
-(hg_hex_pyramid_chain) against one launch per level (HYGRID_PYR_CHAIN=0), interleaved in one
+(hg_hex_pyramid_chain, HYGRID_PYR_CHAIN=1) against one launch per level, interleaved in one
 process on the same buffers, HIP events on the caller's stream around each step; median / min
 of the rounds, outputs compared bit for bit.
     python tools/pyramid_chain_probe.py [rounds] [batch]"""
@@ -30,9 +30,9 @@ def main():
 
     def step(chain):
         if chain:
-            os.environ.pop("HYGRID_PYR_CHAIN", None)
+            os.environ["HYGRID_PYR_CHAIN"] = "1"
         else:
-            os.environ["HYGRID_PYR_CHAIN"] = "0"
+            os.environ.pop("HYGRID_PYR_CHAIN", None)
         return hex_pyramid(x, conv, levels=3, out_dtype=torch.float16)
 
     t = {True: [], False: []}
