@@ -4,7 +4,7 @@ variant three times back to back in a shuffled order and times the last launch; 
 min per launch and the median per-round ratio to the first variant named).
 
 usage: python tools/ab_ops.py OP ROUNDS name1 name2 ...
-  OP: r2h | h2r | conv | wide (HexConv2d 64->64, 1080p bf16 b4) | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1 | pyr2   (bf16 4K b128 for
+  OP: r2h | h2r | conv | wide (HexConv2d 64->64, 1080p bf16 b4) | stem / stem32 (HexConv2d 3->64, 1080p b4, bf16 / f32) | r2h32 | h2r32 | rt | pyr | pyrfr | pyr1 | pyr2   (bf16 4K b128 for
       r2h/h2r/conv; fp32 1080p b32 for r2h32/h2r32 and rt, the fused round trip; pyr = config-5 pyramid level 0, 8K fp16 b8 -> 4K from a
       hex image, pyrfr = the same from the rect image, pyr1 = level 1, 4K -> 2K, pyr2 = level 2, 2K -> 1K;
       hr0 / hr1 / hr2 = hexresize alone at those three levels (fp16); hrb = 4K -> 2K bf16 b32; up = hex (h/2, w/2) -> rect (h, w)
@@ -49,6 +49,8 @@ def main():
         B, C, H, W, t = 32, 3, 1080, 1920, torch.float32
     elif op == "wide":
         B, C, H, W, t = 4, 64, 1080, 1920, torch.bfloat16
+    elif op in ("stem", "stem32"):     # an mmseg stem: HexConv2d(3 -> 64), 1080p b4
+        B, C, H, W, t = 4, 3, 1080, 1920, torch.bfloat16 if op == "stem" else torch.float32
     elif op in ("pyr1", "hr1"):
         B, C, H, W, t = 8, 3, 2160, 3840, torch.float16
     elif op in ("pyr2", "hr2"):
@@ -71,11 +73,14 @@ def main():
         y = torch.empty((B, C, H // 2, W // 2), device=dev, dtype=t)
     elif op in ("up", "upn"):
         y = torch.empty((B, C, 2 * H, 2 * W), device=dev, dtype=t)
+    elif op in ("stem", "stem32"):
+        y = torch.empty((B, 64, H, W), device=dev, dtype=t)
     else:
         y = torch.empty_like(x)
     kc = C if op == "wide" else 3
-    k = (torch.rand((kc, 7 * kc), generator=g, device=dev) - 0.5) * (0.5 if kc == 3 else 0.05)
-    b = torch.rand((kc,), generator=g, device=dev) - 0.5
+    ko = 64 if op in ("stem", "stem32") else kc
+    k = (torch.rand((ko, 7 * kc), generator=g, device=dev) - 0.5) * (0.5 if kc == 3 else 0.05)
+    b = torch.rand((ko,), generator=g, device=dev) - 0.5
     s = st.cuda_stream
 
     def call(lib):
@@ -100,11 +105,11 @@ def main():
             f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 5 + [_int, _vp]
             return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B * C, H, W, 2 * H, 2 * W,
                      0 if op == "upn" else 1, s)
-        if op in ("conv", "wide"):
+        if op in ("conv", "wide", "stem", "stem32"):
             f = lib.hg_hexconv2d
             f.argtypes = [_vp] * 4 + [_int] * 3 + [_i64] * 5 + [_int] * 7 + [_dbl, _vp]
             return f(x.data_ptr(), k.data_ptr(), b.data_ptr(), y.data_ptr(), dt[t], _abi.HG_F32,
-                     dt[t], B, C, C, H, W, 2, 1, 1, 1, 1, 0, 0, 0.0, s)
+                     dt[t], B, C, ko, H, W, 2, 1, 1, 1, 1, 0, 0, 0.0, s)
         f = lib.hg_hex_pyramid_level
         f.argtypes = [_vp, _vp, _int, _int] + [_i64] * 6 + [_vp, _vp, _int, _int, _vp]
         return f(x.data_ptr(), y.data_ptr(), dt[t], dt[t], B, C, H, W, H // 2, W // 2,
@@ -113,6 +118,7 @@ def main():
     times = {n: [] for n in names}
     ratios = {n: [] for n in names}
     sums = {}
+    outs = {}
     rng = random.Random(7)
     for r in range(rounds + 1):
         order = list(libs.items())
@@ -135,6 +141,8 @@ def main():
             rt[n] = e0.elapsed_time(e1)
             if r == rounds:
                 sums[n] = float(y.double().sum().item())
+                if op in ("stem", "stem32"):       # element-wise against the first variant named
+                    outs[n] = y.float().clone()
         if r > 0:
             for n in names:
                 times[n].append(rt[n])
@@ -145,6 +153,11 @@ def main():
         print(f"{op:6s} {n:14s} median {statistics.median(tm):.4f} ms  min {min(tm):.4f} ms  "
               f"{alg / statistics.median(tm) / 1e6:.0f} GB/s  vs {names[0]} "
               f"{statistics.median(ratios[n]):.4f}  checksum {sums[n]:.9e}", flush=True)
+    if outs:
+        ref = outs[names[0]]
+        for n in names[1:]:
+            d = (outs[n] - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)
+            print(f"{op:6s} {n:14s} max |diff| / max |{names[0]}| = {d:.3e}", flush=True)
 
 
 if __name__ == "__main__":
