@@ -753,6 +753,33 @@ def main():
                                      "the algorithm's own ceiling is 2500 / 3 / (8/7) = 729 "
                                      "TFLOP/s of fp32-exact conv"}}
         del xw
+        # the 3-channel stem of the same model, HexConv2d(3, 64) on the 1080p bf16 batch (round
+        # 6: on the bf16 MFMA kernel with its channel chunk zero-padded, was the generic kernel):
+        # bytes = input + 64-channel output, TFLOP/s on the algorithmic 2 * O * 7 * C
+        Cs = 3
+        xs_ = (torch.rand((Bw, Cs, Hw, Ww), generator=gen, device=dev) - 0.5).to(bf16)
+        torch.manual_seed(6)
+        sconv = HexConv2d(Cs, Ow, 0, 2, padding=1, bias=True).to(dev)
+        sconv.out_dtype = bf16
+
+        def run_stem(record, ev):
+            if record:
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                e[0].record()
+            out = sconv(xs_)
+            if record:
+                e[1].record()
+                ev.append(e)
+            return out
+
+        _, _, sms_s = measure_line(run_stem, steps_w)
+        sb = 2.0 * Bw * Hw * Ww * (Cs + Ow)
+        wide["stem"] = {"workload": f"HexConv2d({Cs},{Ow},0,2,padding=1) bf16, {Bw}x{Cs}x{Hw}x{Ww}",
+                        "ms": round(sms_s[0], 4), "alg_GB": round(sb / 1e9, 4),
+                        "GB_per_s": round(sb / (sms_s[0] * 1e-3) / 1e9, 1),
+                        "frac_of_peak": round(sb / (sms_s[0] * 1e-3) / PEAK_BPS, 4),
+                        "TFLOP_s": round(2.0 * Ow * 7 * Cs * Bw * Hw * Ww / (sms_s[0] * 1e-3) / 1e12, 2)}
+        del xs_
 
     lattices = None
     if not args.unfused and not dry and not args.no_lattices:

@@ -613,14 +613,18 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
 }
 
 // Runs the MFMA kernel when it covers the call and pays (dense radius-2, stride-1,
-// dilation-1 conv with C >= 8 and O >= 16, f32 weights); HG_EUNSUP otherwise.
+// dilation-1 conv with O >= 16, f32 weights); HG_EUNSUP otherwise.  Narrow inputs (C < 8: the
+// 3-channel stem of a segmentation model, HexModules.py:97-288) run here too, their channel
+// chunk padded with zeros (staging and weights read 0 past C): HexConv2d(3 -> 64) 1080p b4
+// 2.76 -> 0.50 ms (bf16) and 2.84 -> 1.02 ms (f32) against the generic kernel, round 6,
+// profiles/r06/stem_conv_ab.txt.
 int conv_mfma_try(const void* x, const float* k, const float* b, void* y, int x_dtype,
                   int y_dtype, int64_t B, int64_t C, int64_t O, int64_t h, int64_t w, int radius,
                   int stride, int padding, int dilation, int groups, int off, int pad_mode,
                   double pad_value, const Epilogue& epi, hipStream_t st) {
     if (env_is("HYGRID_CONV_MFMA", "0")) return HG_EUNSUP;   // A/B switch: generic kernels
     if (radius != 2 || stride != 1 || dilation != 1 || groups != 1) return HG_EUNSUP;
-    if (C < 8 || O < 16 || padding < 0 || padding > 2) return HG_EUNSUP;
+    if (C < 1 || O < 16 || padding < 0 || padding > 2) return HG_EUNSUP;
     if (C > INT_MAX / 16 || O > INT_MAX / 16 || h > INT_MAX / 4 || w > INT_MAX / 4) return HG_EUNSUP;
     if (C * h * w * 4 >= ((int64_t)1 << 31)) return HG_EUNSUP;   // 32-bit buffer offsets
     MfmaGeom G = {};

@@ -1,5 +1,5 @@
 """GPU parity of the wide-channel HexConv2d path (csrc/conv_mfma.hip: implicit GEMM on
-v_mfma_f32_16x16x4_f32, dense radius 2 / stride 1 / dilation 1, C >= 8, O >= 16) against
+v_mfma_f32_16x16x4_f32, dense radius 2 / stride 1 / dilation 1, O >= 16; C < 8 zero-padded) against
 the fp64 oracle (oracle/hg_oracle.c, pinned to HexFrames.py:96-169 by
 tests/golden/hexconv.npz) at the north_star fp32 tolerance (rtol 1e-5, atol 1e-5*max|ref|),
 and against the generic LDS kernel (HYGRID_CONV_MFMA=0) for 16-bit outputs and the fused
@@ -47,6 +47,8 @@ def _weights(O_, C, seed):
 CASES = [  # (B, C, O, h, w)
     (2, 8, 16, 9, 10), (1, 16, 16, 33, 70), (1, 32, 64, 20, 130), (2, 64, 64, 17, 64),
     (1, 13, 20, 12, 21), (1, 24, 100, 11, 75), (1, 70, 33, 6, 9),
+    # narrow inputs (round 6): a 3-channel stem, 1 and 5 channels (zero-padded chunk)
+    (2, 3, 64, 20, 130), (1, 1, 16, 9, 10), (1, 5, 40, 14, 33),
 ]
 
 
@@ -245,7 +247,7 @@ def _with_env(name, value, fn, *args, **kw):
 
 DMA_CASES = [  # (B, C, O, h, w): interior tiles (DMA-staged P) and border tiles in each
     (1, 64, 64, 40, 300), (2, 13, 20, 30, 260), (1, 70, 33, 17, 202), (1, 24, 100, 21, 196),
-    (1, 8, 16, 12, 140)]
+    (1, 8, 16, 12, 140), (1, 3, 64, 30, 260), (2, 1, 16, 12, 140)]
 
 
 @pytest.mark.parametrize("case", DMA_CASES)

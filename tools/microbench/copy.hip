@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
 __global__ __launch_bounds__(256) void copy_gs(const float4* __restrict__ x, float4* __restrict__ y, int64_t n) {
@@ -62,8 +63,10 @@ float timeit(K k, int reps) {
     return ms / reps;
 }
 
-int main() {
-    const size_t bytes = (size_t)128 * 3 * 2160 * 3840 * 2;
+// usage: copy [bytes per side]   (default: the headline's 6.37 GB; config 2's 1080p fp32 b32
+// round trip moves 796262400 per side)
+int main(int argc, char** argv) {
+    const size_t bytes = argc > 1 ? (size_t)atoll(argv[1]) & ~(size_t)15 : (size_t)128 * 3 * 2160 * 3840 * 2;
     const int64_t n = (int64_t)(bytes / 16);
     float4 *x, *y;
     CK(hipMalloc(&x, bytes)); CK(hipMalloc(&y, bytes));
