@@ -41,6 +41,9 @@ constexpr int CM_CST = CM_PR * CM_PP;       // P channel stride
 constexpr int CM_WST = 7 * CM_OMAX + 16;    // weight channel stride (= 16 mod 32 banks)
 
 typedef float cm_f4 __attribute__((ext_vector_type(4)));
+#ifndef CM_TD
+#define CM_TD 1                             // k_hexconv_mfma_bf16d: D as [column][channel] (below)
+#endif
 
 struct MfmaGeom {
     int64_t B;
@@ -439,12 +442,15 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
                           px0 + CB_PP - 1 < G.w && q0 + G.mink + CB_PP - 1 < Wp;
     const int xs = px0 & ~1, sh = px0 - xs;               // dword-aligned raw start, shift
 
+    // CM_TD: the MFMAs take the P fragment as A and the weights as B, so D is [column][channel]:
+    // a lane's 4 registers are 4 adjacent output columns of one channel (one 8-B store for
+    // 16-bit outputs instead of four 2-B stores); the same products summed in the same order
     cm_f4 acc[NOT][NQT];
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-            const int o = o0 + ot * 16 + lg * 4 + v;
+            const int o = o0 + ot * 16 + (CM_TD ? li : lg * 4 + v);
             const float bv = (bias && o < G.O) ? bias[o] : 0.f;
 #pragma unroll
             for (int qt = 0; qt < NQT; ++qt) acc[ot][qt][v] = bv;
@@ -584,7 +590,8 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
                     const cm_b8 af = __builtin_bit_cast(cm_b8, wsb[((pt * 2 + kb) * CM_O + ot * 16 + li) * 4 + cd_wslot(li, lg)]);
 #pragma unroll
                     for (int qt = 0; qt < NQT; ++qt)
-                        acc[ot][qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[qt], acc[ot][qt], 0, 0, 0);
+                        acc[ot][qt] = CM_TD ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[qt], af, acc[ot][qt], 0, 0, 0)
+                                            : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[qt], acc[ot][qt], 0, 0, 0);
                 }
             }
         }
@@ -595,6 +602,36 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
 
     if (r >= G.ho) return;
     Tout* yb = y + b * (int64_t)G.O * G.ho * G.wo;
+    if constexpr (CM_TD) {
+        // 16-bit outputs with wo % 4 == 0: 4 columns per 8-B store (8-B aligned: q % 4 == 0)
+        const bool vec = sizeof(Tout) == 2 && (G.wo & 3) == 0;
+#pragma unroll
+        for (int ot = 0; ot < NOT; ++ot) {
+            const int o = o0 + ot * 16 + li;
+            if (o >= G.O) continue;
+#pragma unroll
+            for (int qt = 0; qt < NQT; ++qt) {
+                const int q = q0 + qt * 16 + lg * 4;
+                if (q >= G.wo) continue;
+                float val[4];
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    val[v] = acc[ot][qt][v];
+                    if (G.epi.on) val[v] = epi_apply(val[v], o, G.epi);
+                }
+                Tout* const dst = yb + ((int64_t)o * G.ho + r) * G.wo + q;
+                if (vec) {
+                    typedef Tout t4v __attribute__((ext_vector_type(4)));
+                    *reinterpret_cast<t4v*>(dst) = t4v{(Tout)val[0], (Tout)val[1], (Tout)val[2], (Tout)val[3]};
+                } else {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        if (q + v < G.wo) dst[v] = (Tout)val[v];
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
