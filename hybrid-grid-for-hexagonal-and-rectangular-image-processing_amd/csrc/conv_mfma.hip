@@ -42,7 +42,7 @@ constexpr int CM_WST = 7 * CM_OMAX + 16;    // weight channel stride (= 16 mod 3
 
 typedef float cm_f4 __attribute__((ext_vector_type(4)));
 #ifndef CM_TD
-#define CM_TD 1                             // k_hexconv_mfma_bf16d: D as [column][channel] (below)
+#define CM_TD 1                             // MFMA kernels, 16-bit outputs: D as [column][channel] (below)
 #endif
 
 struct MfmaGeom {
@@ -54,6 +54,40 @@ struct MfmaGeom {
     float pad_value;
     Epilogue epi;
 };
+
+// CM_TD epilogue (16-bit outputs): lane (li, lk) holds output channel oc + 16 ot, columns
+// q + 16 qt .. + 3 in its 4 registers: one 8-B store per (ot, qt) when every row's start keeps
+// q % 4 == 0 aligned (wo % 4 == 0); scalar stores otherwise
+template <typename Tout, int NOT, int NQT>
+__device__ __forceinline__ void cm_store_cols(const cm_f4 (&acc)[NOT][NQT], Tout* yb, const MfmaGeom& G,
+                                              int oc, int q, int r) {
+    const bool vec = (G.wo & 3) == 0;
+#pragma unroll
+    for (int ot = 0; ot < NOT; ++ot) {
+        const int o = oc + ot * 16;
+        if (o >= G.O) continue;
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt) {
+            const int qq = q + qt * 16;
+            if (qq >= G.wo) continue;
+            float val[4];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                val[v] = acc[ot][qt][v];
+                if (G.epi.on) val[v] = epi_apply(val[v], o, G.epi);
+            }
+            Tout* const dst = yb + ((int64_t)o * G.ho + r) * G.wo + qq;
+            if (vec && sizeof(Tout) == 2) {
+                typedef Tout t4v __attribute__((ext_vector_type(4)));
+                *reinterpret_cast<t4v*>(dst) = t4v{(Tout)val[0], (Tout)val[1], (Tout)val[2], (Tout)val[3]};
+            } else {
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    if (qq + v < G.wo) dst[v] = (Tout)val[v];
+            }
+        }
+    }
+}
 
 template <typename Tin, typename Tout, int NOT>
 __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma(const Tin* __restrict__ x,
@@ -76,12 +110,15 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma(const Tin* __restri
     const int Wp = G.w + 2 * G.p, Hp = G.h + 2 * G.p;
     const int li = lane & 15, lk = lane >> 4;            // fragment row / k of this lane
 
+    // 16-bit outputs only (fp32 outputs as two 8-B stores: 3.9 % slower than 2-B stores,
+    // profiles/r06/conv_mfma_transposed_d_ab.txt)
+    constexpr bool TD = CM_TD && sizeof(Tout) == 2;
     cm_f4 acc[NOT][4];
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-            const int o = o0 + ot * 16 + lk * 4 + v;
+            const int o = o0 + ot * 16 + (TD ? li : lk * 4 + v);   // TD: D is [column][channel]
             const float bv = (bias && o < G.O) ? bias[o] : 0.f;
 #pragma unroll
             for (int qt = 0; qt < 4; ++qt) acc[ot][qt][v] = bv;
@@ -158,8 +195,8 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma(const Tin* __restri
                 for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
                     for (int qt = 0; qt < 4; ++qt)
-                        acc[ot][qt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[ot], bf[qt],
-                                                                           acc[ot][qt], 0, 0, 0);
+                        acc[ot][qt] = TD ? __builtin_amdgcn_mfma_f32_16x16x4f32(bf[qt], af[ot], acc[ot][qt], 0, 0, 0)
+                                            : __builtin_amdgcn_mfma_f32_16x16x4f32(af[ot], bf[qt], acc[ot][qt], 0, 0, 0);
             }
         }
         __syncthreads();
@@ -168,6 +205,10 @@ __global__ __launch_bounds__(CM_THREADS) void k_hexconv_mfma(const Tin* __restri
     // ---- epilogue: bias was the accumulator's start; BN / activation; store -------------
     if (r >= G.ho) return;
     Tout* yb = y + b * (int64_t)G.O * G.ho * G.wo;
+    if constexpr (TD) {
+        cm_store_cols<Tout, NOT, 4>(acc, yb, G, o0 + li, q0 + lk * 4, r);
+        return;
+    }
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot)
 #pragma unroll
@@ -445,12 +486,15 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
     // CM_TD: the MFMAs take the P fragment as A and the weights as B, so D is [column][channel]:
     // a lane's 4 registers are 4 adjacent output columns of one channel (one 8-B store for
     // 16-bit outputs instead of four 2-B stores); the same products summed in the same order
+    // 16-bit outputs only (fp32 outputs as two 8-B stores: 3.9 % slower than 2-B stores,
+    // profiles/r06/conv_mfma_transposed_d_ab.txt)
+    constexpr bool TD = CM_TD && sizeof(Tout) == 2;
     cm_f4 acc[NOT][NQT];
 #pragma unroll
     for (int ot = 0; ot < NOT; ++ot) {
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-            const int o = o0 + ot * 16 + (CM_TD ? li : lg * 4 + v);
+            const int o = o0 + ot * 16 + (TD ? li : lg * 4 + v);
             const float bv = (bias && o < G.O) ? bias[o] : 0.f;
 #pragma unroll
             for (int qt = 0; qt < NQT; ++qt) acc[ot][qt][v] = bv;
@@ -590,7 +634,7 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
                     const cm_b8 af = __builtin_bit_cast(cm_b8, wsb[((pt * 2 + kb) * CM_O + ot * 16 + li) * 4 + cd_wslot(li, lg)]);
 #pragma unroll
                     for (int qt = 0; qt < NQT; ++qt)
-                        acc[ot][qt] = CM_TD ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[qt], af, acc[ot][qt], 0, 0, 0)
+                        acc[ot][qt] = TD ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[qt], af, acc[ot][qt], 0, 0, 0)
                                             : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[qt], acc[ot][qt], 0, 0, 0);
                 }
             }
@@ -602,34 +646,8 @@ void k_hexconv_mfma_bf16d(const __bf16* __restrict__ x,
 
     if (r >= G.ho) return;
     Tout* yb = y + b * (int64_t)G.O * G.ho * G.wo;
-    if constexpr (CM_TD) {
-        // 16-bit outputs with wo % 4 == 0: 4 columns per 8-B store (8-B aligned: q % 4 == 0)
-        const bool vec = sizeof(Tout) == 2 && (G.wo & 3) == 0;
-#pragma unroll
-        for (int ot = 0; ot < NOT; ++ot) {
-            const int o = o0 + ot * 16 + li;
-            if (o >= G.O) continue;
-#pragma unroll
-            for (int qt = 0; qt < NQT; ++qt) {
-                const int q = q0 + qt * 16 + lg * 4;
-                if (q >= G.wo) continue;
-                float val[4];
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    val[v] = acc[ot][qt][v];
-                    if (G.epi.on) val[v] = epi_apply(val[v], o, G.epi);
-                }
-                Tout* const dst = yb + ((int64_t)o * G.ho + r) * G.wo + q;
-                if (vec) {
-                    typedef Tout t4v __attribute__((ext_vector_type(4)));
-                    *reinterpret_cast<t4v*>(dst) = t4v{(Tout)val[0], (Tout)val[1], (Tout)val[2], (Tout)val[3]};
-                } else {
-#pragma unroll
-                    for (int v = 0; v < 4; ++v)
-                        if (q + v < G.wo) dst[v] = (Tout)val[v];
-                }
-            }
-        }
+    if constexpr (TD) {
+        cm_store_cols<Tout, NOT, NQT>(acc, yb, G, o0 + li, q0 + lg * 4, r);
         return;
     }
 #pragma unroll
