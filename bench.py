@@ -43,13 +43,14 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# What bounds the headline kernel (DESIGN.md section 6, round 5 measurements): its
-# cache-resident build (every load / store hits one row) runs 1.83-2.02 ms, the real one
-# ~0.7 ms more; loads alone or stores alone add ~0.25 ms each, both together ~0.7 ms.
-FUSED4_LIMITER = ("memory latency on top of VALU issue (k_fused4: 136 VGPRs, 3 waves per SIMD, "
-                  "2 rect rows of prefetch): cache-resident floor 1.83-2.02 ms per 4K b128 launch, "
-                  "the interleaved row-load / row-store stream adds ~0.6 ms that does not "
-                  "overlap with the stencil; the same walk with no arithmetic reaches 0.57 of "
+# What bounds the headline kernel (rounds 5-6): its cache-resident build
+# (every load / store hits one row) runs 1.83-2.02 ms, the real one ~0.6-0.7 ms more; loads
+# alone or stores alone add ~0.25 ms each, both together ~0.7 ms; bytes are 1.035x (round 6).
+FUSED4_LIMITER = ("the streaming rate of the band walk on top of VALU issue (k_fused4: 136 VGPRs, "
+                  "3 waves per SIMD, 2 rect rows of prefetch): HBM traffic is 1.035x the "
+                  "algorithmic bytes (round 6), the cache-resident floor 1.83-2.02 ms per 4K b128 "
+                  "launch, and the interleaved row-load / row-store stream adds ~0.6 ms that does "
+                  "not overlap with the stencil; the same walk with no arithmetic reaches 0.57 of "
                   "8 TB/s, 0.65 with a store wave (profiles/r05/fused4_floor_ab.txt, "
                   "fused4_additivity_ab.txt, profiles/r06/walk9_store_wave.txt)")
 PEAK_BPS = HBM_PEAK_GBS * 1e9
