@@ -398,22 +398,8 @@ def main():
 
     from HyGrid.dist import gather_sums
     sums_buf = {}
-    # the per-step reduction + all-gather run on a side stream that waits for the step's
-    # kernel, so they overlap the next step's kernel instead of extending the step (round 6;
-    # the timed region ends with a device-wide synchronize, so the last step's collective is
-    # inside it).  y.record_stream keeps the caching allocator from reusing y's memory for a
-    # later step's output before the side stream has read it.
-    side = None if dry else torch.cuda.Stream(device=dev)
 
     def step_sums(y):
-        if side is None:
-            return step_sums_(y)
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            y.record_stream(side)
-            step_sums_(y)
-
-    def step_sums_(y):
         """Per-image, per-channel sums of every 256th output row, all-gathered over RCCL: the
         collective every timed step ends with (a few KB per rank), at every N (N = 1: the
         world-1 group).  Row sums first (contiguous inner reduction), then over the sampled
