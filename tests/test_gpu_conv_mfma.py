@@ -115,6 +115,27 @@ def test_mfma_hexconvmodule_epilogue_vs_generic(act):
     torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 64, 24, 100), (1, 3, 32, 17, 37), (1, 16, 48, 9, 38)])
+@pytest.mark.parametrize("dt_in", [torch.bfloat16, torch.float16])
+def test_mfma_column_store_epilogue_vs_generic(shape, dt_in):
+    """16-bit outputs take the [column][channel] accumulator and its 8-B column stores (round 6,
+    CM_TD), widths that are not a multiple of 4 its scalar stores; with the fused BN-affine +
+    LeakyReLU epilogue on both kernels (bf16 in: the DMA kernel, f16 in: the f32-MFMA kernel)."""
+    B, C, O_, h, w = shape
+    k, b = _weights(O_, C, 21 + w)
+    g = torch.Generator(device=DEV).manual_seed(w)
+    x = (torch.rand((B, C, h, w), generator=g, device=DEV) - 0.5).to(dt_in)
+    scale = torch.rand((O_,), generator=g, device=DEV) + 0.5
+    shift = torch.rand((O_,), generator=g, device=DEV) - 0.5
+    epi = (scale, shift, 2, 0.1)          # hg_act 2: LeakyReLU
+    for od in (dt_in, torch.float32):
+        y = ops.hexconv2d(x, k, b, 0, 2, padding=1, out_dtype=od, epilogue=epi)
+        ref = _generic(ops.hexconv2d, x, k, b, 0, 2, padding=1, out_dtype=od, epilogue=epi)
+        ulp = {torch.bfloat16: 2.0 ** -8, torch.float16: 2.0 ** -11, torch.float32: 1e-5}[od]
+        sc = float(ref.float().abs().max())
+        torch.testing.assert_close(y.float(), ref.float(), rtol=ulp, atol=ulp * sc)
+
+
 def test_mfma_conv_nan_positions_match_generic():
     B, C, O_, h, w = 1, 16, 16, 20, 70
     k, b = _weights(O_, C, 4)
